@@ -1,0 +1,234 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+numpy restatement of the reference codecs and reduction, op for op in fp32:
+
+* ``parse_spec`` / ``OracleCompressor.__init__``  — initCompressor, compressors.py:435-494,
+  and the make* constructors, compressors.py:64-178.
+* ``OracleCompressor.generate``  — generateCompressPattern, compressors.py:196-216.
+* ``OracleCompressor.compress``  — compressVector, compressors.py:218-371 (rank_k excluded:
+  a dense SVD, SURVEY §8f, not on this round's path).
+* ``server_gradient``            — serverGradient core, algorithms.py:1748-1770 (DCGD) and
+  1810-1832 (FedAvg): gs = w0 (x - x0); gs += wi (x - xi) in buffer order; gs / sum(w).
+* ``reduce_plain``               — the fused encode+reduce contract of the product:
+  the same sequential fp32 sum over already-encoded rows (sum_i wi * C(g_i)) / sum(w).
+
+fp32 semantics reproduced (checked against tests/golden/ fixtures from the real reference):
+  * python-float scalars multiply / divide fp32 tensors as fp32 scalars (torch CPU rule);
+  * dithering compares the float64 uniforms with the fp32 probability promoted to float64
+    (compressors.py:288);  later level intervals overwrite earlier ones (290-291);
+  * ``out * sign * pnorm`` is evaluated left to right in fp32 (296);
+  * natural dithering returns ``y * sign * pnorm`` — the reference's own bug (326);
+  * torch's CPU ``norm`` sums in an implementation-defined fp32 order (up to hundreds of
+    ulp from the exact value at D ~ 1e6); the oracle computes the norm exactly (float64
+    accumulation, one rounding) unless the caller passes the reference's value.
+  * TopK ties at the K-th magnitude are broken by lowest index (torch leaves it unspecified).
+"""
+import math
+
+import numpy as np
+
+IDENTICAL, LAZY, RANDK, NATURAL, STD_DITHERING, NAT_DITHERING, TOPK, RANK_K = range(1, 9)
+_F32 = np.float32
+
+
+def _levels_std(levels):
+    # torch.arange(0.0, 1.0 + 1.0/levels*0.5, 1.0/levels) (compressors.py:87): fp32 values of
+    # start + i*step computed in double, the length ceil((end-start)/step).
+    step = 1.0 / levels
+    end = 1.0 + step * 0.5
+    n = int(math.ceil((end - 0.0) / step))
+    return np.array([0.0 + i * step for i in range(n)], dtype=np.float64).astype(_F32)
+
+
+def _levels_nat(levels):
+    # compressors.py:116-119: zeros(levels+1); [i] = 0.5**i for i < levels; flip.
+    v = np.zeros(levels + 1, dtype=_F32)
+    for i in range(levels):
+        v[i] = _F32(0.5 ** i)
+    return v[::-1].copy()
+
+
+class OracleCompressor:
+    def __init__(self, spec, D):
+        params = spec.split(":")
+        name = params[0]
+        self.D = D
+        self.K = None
+        self.testp = None
+        self.S = None
+        self.total_input_components = 0
+        self.really_need_to_send_components = 0
+        self.last_input_advance = 0
+        self.last_need_to_send_advance = 0
+
+        def kspec(arg):
+            if arg.find("%") == -1:
+                return math.ceil(float(arg))
+            return math.ceil(float(arg[0:-1]) / 100.0 * D)
+
+        def pspec():
+            if len(params) == 3:
+                return math.inf if params[2].lower() == "inf" else int(params[2])
+            return math.inf
+
+        if name == "ident":
+            self.type, self.w = IDENTICAL, 0.0
+        elif name == "randk":
+            self.type, self.K = RANDK, kspec(params[1])
+            self.w = D / self.K - 1.0
+        elif name == "bernulli":
+            self.type, self.P = LAZY, float(params[1])
+            self.w = 1.0 / self.P - 1.0
+        elif name == "natural":
+            self.type, self.w = NATURAL, 1.0 / 8.0
+        elif name in ("qsgd", "std.dithering", "terngrad"):
+            if name == "terngrad":
+                L, p = 1, math.inf
+            elif name == "qsgd":
+                L, p = int(params[1]), 2
+            else:
+                L, p = int(params[1]), pspec()
+            self.type = STD_DITHERING
+            self.levels = _levels_std(L)
+            self.s = len(self.levels) - 1
+            assert self.s == L
+            self.p = p
+            if name == "qsgd":
+                self.w = min(D / (L * L), D ** 0.5 / L)
+            else:
+                self.w = 0.0
+        elif name == "nat.dithering":
+            L, p = int(params[1]), pspec()
+            self.type = NAT_DITHERING
+            self.levels = _levels_nat(L)
+            self.s = L
+            self.p = p
+            r = min(p, 2)
+            self.w = 1.0 / 8.0 + (D ** (1.0 / r)) / (2 ** (self.s - 1)) * min(1, (D ** (1.0 / r)) / (2 ** (self.s - 1)))
+        elif name == "topk":
+            self.type, self.K = TOPK, kspec(params[1])
+            self.alpha = self.K / D
+        else:
+            raise AssertionError("Unknown compressor format")   # compressors.py:492
+
+    # compressors.py:196-216
+    def generate(self, rs):
+        t = self.type
+        if t == LAZY:
+            self.testp = rs.random()
+        elif t == RANDK:
+            self.S = rs.choice(self.D, self.K, replace=False)
+        elif t in (NATURAL, STD_DITHERING, NAT_DITHERING):
+            self.testp = rs.rand(self.D)
+
+    def norm(self, x):
+        if self.p == math.inf:
+            return _F32(np.max(np.abs(x))) if x.size else _F32(0)
+        if self.p == 2:
+            return _F32(np.sqrt(np.sum(x.astype(np.float64) ** 2)))
+        if self.p == 1:
+            return _F32(np.sum(np.abs(x).astype(np.float64)))
+        return _F32(np.sum(np.abs(x).astype(np.float64) ** self.p) ** (1.0 / self.p))
+
+    # compressors.py:218-371
+    def compress(self, x, pnorm=None):
+        x = np.asarray(x, dtype=_F32)
+        d = max(x.shape)
+        t = self.type
+        need = 0
+        with np.errstate(all="ignore"):
+            if t == IDENTICAL:
+                out, need = x, d
+            elif t == LAZY:
+                if self.testp < self.P:
+                    out, need = x / _F32(self.P), d
+                else:
+                    out, need = np.zeros_like(x), 0
+            elif t == RANDK:
+                out = np.zeros_like(x)
+                out[self.S] = _F32(self.D / self.K) * x[self.S]
+                need = self.K
+            elif t == NATURAL:
+                out = np.zeros_like(x)
+                sign = np.sign(x)
+                ax = np.abs(x)
+                alpha = np.log2(ax)
+                lo, hi = np.floor(alpha), np.ceil(alpha)
+                p_lo, p_hi = np.exp2(lo), np.exp2(hi)
+                pt = (p_hi - ax) / p_lo
+                down = self.testp < pt.astype(np.float64)
+                out[down] = (sign * p_lo)[down]
+                out[~down] = (sign * p_hi)[~down]
+                out[x == 0.0] = 0.0
+                need = 9.0 / 32.0 * d
+            elif t in (STD_DITHERING, NAT_DITHERING):
+                pn = self.norm(x) if pnorm is None else _F32(pnorm)
+                out = np.zeros_like(x)
+                sign = np.sign(x)
+                y = np.abs(x) / pn
+                lv = self.levels
+                u = self.testp
+                for s in range(len(lv) - 1):
+                    c12 = (y >= lv[s]) & (y <= lv[s + 1])
+                    p = (y - lv[s + 1]) / (lv[s] - lv[s + 1])
+                    c3 = u < p.astype(np.float64)
+                    out[c12 & c3] = lv[s]
+                    out[c12 & ~c3] = lv[s + 1]
+                out[x == 0.0] = 0.0
+                if t == STD_DITHERING:
+                    out = out * sign * pn
+                else:
+                    out = y * sign * pn
+                need = 1.0 + d * (1.0 + math.ceil(math.log2(self.s))) / 32.0
+            elif t == TOPK:
+                out = np.zeros_like(x)
+                ind = topk_indices(x, self.K)
+                out[ind] = x[ind]
+                need = self.K
+            else:
+                raise NotImplementedError("rank_k is not part of the oracle")
+        self.last_input_advance = d
+        self.last_need_to_send_advance = need
+        self.really_need_to_send_components += need
+        self.total_input_components += d
+        return out
+
+
+def topk_keys(x):
+    """Order-preserving uint32 key of |x| (NaN above +inf, like torch.topk)."""
+    return (np.asarray(x, dtype=_F32).view(np.uint32) & np.uint32(0x7FFFFFFF))
+
+
+def topk_indices(x, K):
+    """Indices of the K largest |x|, ties at the K-th magnitude broken by lowest index."""
+    key = topk_keys(x).astype(np.int64)
+    order = np.lexsort((np.arange(key.size), -key))
+    return np.sort(order[:K])
+
+
+def server_gradient(x, models, weights=None):
+    """algorithms.py:1753-1768: sequential fp32, python-float weights applied as fp32."""
+    x = np.asarray(x, dtype=_F32)
+    n = len(models)
+    if n == 0:
+        return np.zeros_like(x)                          # algorithms.py:2117-2118
+    w = [1.0] * n if weights is None else [float(v) for v in weights]
+    gs = _F32(w[0]) * (x - np.asarray(models[0], dtype=_F32))
+    wt = w[0]
+    for i in range(1, n):
+        gi = x - np.asarray(models[i], dtype=_F32)
+        wt += w[i]
+        gs = gs + _F32(w[i]) * gi
+    return gs / _F32(wt)
+
+
+def reduce_plain(rows, weights=None):
+    """(sum_i w_i * row_i) / sum(w), sequential fp32 in row order (fused encode+reduce contract)."""
+    n = len(rows)
+    w = [1.0] * n if weights is None else [float(v) for v in weights]
+    gs = _F32(w[0]) * np.asarray(rows[0], dtype=_F32)
+    wt = w[0]
+    for i in range(1, n):
+        wt += w[i]
+        gs = gs + _F32(w[i]) * np.asarray(rows[i], dtype=_F32)
+    return gs / _F32(wt)

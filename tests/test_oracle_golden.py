@@ -1,0 +1,153 @@
+"""Pin the oracle (oracle/) against the real reference's outputs (tests/golden/)."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import codecs as oc
+from oracle.rng import OracleRandomState
+from tests.golden_io import load
+
+CODEC_META, CODEC = load("codecs")
+RNG_META, RNG = load("rng")
+RUN_META, RUNS = load("runs")
+
+
+@pytest.mark.parametrize("i", range(len(RNG_META)))
+def test_rng_stream(i):
+    m = RNG_META[i]
+    rs = OracleRandomState(m["seed"])
+    want = RNG[f"r{i:02d}"]
+    if m["kind"] == "choice":
+        got = rs.choice(m["args"][0], m["args"][1])
+    elif m["kind"] == "rand":
+        got = rs.rand(m["args"][0])
+    elif m["kind"] == "random":
+        got = np.array([rs.random() for _ in range(m["args"][0])])
+    elif m["kind"] == "randint31":
+        got = np.array([rs.randint31() for _ in range(m["args"][0])])
+    else:  # interleaved DCGD-like sequence
+        vals = []
+        for _ in range(2):
+            vals.extend(rs.choice(10, 4).tolist())
+        for _ in range(4):
+            vals.extend(rs.choice(2465, 247).tolist())
+            vals.append(rs.randint31())
+        vals.extend(rs.rand(3).view(np.int64).tolist())
+        got = np.array(vals, dtype=np.int64)
+    np.testing.assert_array_equal(got, want)
+    key, pos = rs.state()
+    assert pos == m["end_pos"]
+    np.testing.assert_array_equal(key[:8], RNG[f"r{i:02d}_endkey"])
+
+
+def _case(i):
+    m = CODEC_META[i]
+    return m, CODEC[f"c{i:02d}_x"], CODEC[f"c{i:02d}_out"]
+
+
+@pytest.mark.parametrize("i", range(len(CODEC_META)))
+def test_codec_constants(i):
+    m = CODEC_META[i]
+    c = oc.OracleCompressor(m["spec"], m["D"])
+    assert c.type == m["type"]
+    assert c.K == m["K"]
+    assert getattr(c, "w", None) == m["w"]
+    assert getattr(c, "alpha", None) == m["alpha"]
+    if m["type"] in (5, 6):
+        np.testing.assert_array_equal(c.levels, CODEC[f"c{i:02d}_levels"])
+        assert c.s == m["s"] and float(c.p) == m["p"]
+
+
+@pytest.mark.parametrize("i", range(len(CODEC_META)))
+def test_codec_outputs(i):
+    """Bit-exact outputs, patterns and stats; dithering given the reference's own norm."""
+    m, X, OUT = _case(i)
+    rs = OracleRandomState(m["seed"])
+    stats = CODEC[f"c{i:02d}_stats"]
+    pn = CODEC[f"c{i:02d}_pnorm"]
+    for c in range(m["n_clients"]):
+        comp = oc.OracleCompressor(m["spec"], m["D"])
+        comp.generate(rs)
+        assert rs.randint31() == m["client_seeds"][c]
+        if m["type"] == 3:
+            np.testing.assert_array_equal(comp.S, CODEC[f"c{i:02d}_pat{c}"])
+        if m["type"] == 2:
+            assert comp.testp == CODEC[f"c{i:02d}_pat{c}"][0]
+        if m["type"] in (4, 5, 6) and c == 0 and f"c{i:02d}_pat0" in CODEC.files:
+            np.testing.assert_array_equal(comp.testp, CODEC[f"c{i:02d}_pat0"])
+        x = X[c]
+        if m["type"] == 7:
+            out = comp.compress(x)
+            want = OUT[c]
+            # same nonzero set unless the K-th magnitude ties (reference tie order is torch's)
+            kth = np.sort(oc.topk_keys(x))[::-1][m["K"] - 1] if m["K"] <= x.size else None
+            tied = np.sum(oc.topk_keys(x) == kth) > 1
+            if not tied:
+                np.testing.assert_array_equal(out, want)
+            else:
+                np.testing.assert_array_equal(np.sort(np.abs(out)), np.sort(np.abs(want)))
+        else:
+            out = comp.compress(x, pnorm=(pn[c] if m["type"] in (5, 6) else None))
+            np.testing.assert_array_equal(out.view(np.uint32), OUT[c].view(np.uint32))
+        # per-call stats (compressors.py:223-224, 367-368); a fresh compressor per client
+        assert [comp.total_input_components, comp.really_need_to_send_components,
+                comp.last_input_advance, comp.last_need_to_send_advance] == list(stats[c])
+    assert [rs.randint31() for _ in range(4)] == m["after_draws"]
+
+
+@pytest.mark.parametrize("i", [i for i, m in enumerate(CODEC_META) if m["type"] in (5, 6)])
+def test_dithering_own_norm(i):
+    """With the oracle's own (exactly rounded) norm: outputs equal the reference's up to the
+    norm's scale (torch's CPU fp32 norm is not exactly rounded) and rare level flips."""
+    m, X, OUT = _case(i)
+    rs = OracleRandomState(m["seed"])
+    pn = CODEC[f"c{i:02d}_pnorm"]
+    for c in range(m["n_clients"]):
+        comp = oc.OracleCompressor(m["spec"], m["D"])
+        comp.generate(rs)
+        rs.randint31()
+        mine = comp.norm(X[c])
+        rel = abs(float(mine) / pn[c] - 1.0)
+        assert rel < 64 * 2.0 ** -24 * max(1.0, math.sqrt(m["D"]) / 8)
+        out = comp.compress(X[c])
+        want = OUT[c]
+        ok = np.isclose(out, want, rtol=4 * rel + 4 * 2.0 ** -24, atol=0)
+        assert np.mean(~ok) <= 0.01
+
+
+@pytest.mark.parametrize("name", sorted(RUN_META))
+def test_server_gradient_runs(name):
+    """run.py captures (config C1 + DCGD): the sequential fp32 reduction is bit-exact."""
+    meta = RUN_META[name]
+    for r in range(meta["rounds"]):
+        x = RUNS[f"{name}_r{r}_x"]
+        models = RUNS[f"{name}_r{r}_models"]
+        gs = oc.server_gradient(x, list(models))
+        np.testing.assert_array_equal(gs.view(np.uint32), RUNS[f"{name}_r{r}_gs"].view(np.uint32))
+        # history scalar (algorithms.py:2220), l2_norm_of_vec = sqrt(sum(g**2)) (mutils.py:395)
+        l2 = math.sqrt(float(np.sum(gs.astype(np.float64) ** 2)))
+        assert abs(l2 - meta["grad_sgd_server_l2"][r]) <= 1e-6 * meta["grad_sgd_server_l2"][r]
+        xb = math.sqrt(float(np.sum(x.astype(np.float64) ** 2)))
+        assert abs(xb - meta["x_before_round"][r]) <= 1e-6 * meta["x_before_round"][r]
+        if r + 1 < meta["rounds"]:   # global SGD step, lr 1.0: x <- x - 1.0 * gs (model_funcs.py:605)
+            nxt = x - np.float32(meta["global_lr"]) * gs
+            np.testing.assert_array_equal(nxt, RUNS[f"{name}_r{r+1}_x"])
+
+
+def test_run_patterns_follow_stream():
+    """DCGD randk: the RandK sets drawn inside run.py follow the predicted stream order:
+    seed(runtime) -> per-round client sampling -> per client choice(D,K) then randint(2**31)."""
+    name = "dcgd_randk10"
+    pats = RUNS[f"{name}_patterns"]
+    D = RUN_META[name]["D"]
+    K = math.ceil(0.1 * D)
+    rs = OracleRandomState(456)
+    for _ in range(3):
+        rs.choice(4, 4)
+    k = 0
+    for _ in range(3):
+        for _ in range(4):
+            np.testing.assert_array_equal(rs.choice(D, K), pats[k])
+            rs.randint31()
+            k += 1
