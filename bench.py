@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident gradient-codec encode + N-way reduce on MI355X.
+
+BASELINE.json metric: "gradient-codec encode+reduce GB/s (device-resident), [N,D] fp32; % HBM peak".
+
+A step = one simulated uplink: every client row of the resident synthetic [N, D] fp32 matrix is
+encoded with its codec and the rows are reduced to one [D] direction (flc_encode_reduce, one
+call); with --gpus G > 1 every rank holds its own N-row shard (weak scaling, one process per GPU)
+and the [D] partial sums are combined with one RCCL all-reduce over xGMI, then divided by the
+global client count.
+
+Workloads (BASELINE.json configs; the default is the largest single-GPU config, C3):
+  c3  topk:1%   N=1024 / GPU, D=10 M   (ResNet-18-sized)                     [default]
+  c2  randk:1%  N=256  / GPU, D=1 M    (device-RNG indices)
+  c4  qsgd:127  N=512  / GPU, D=25 M   (C4's per-GPU shard: at --gpus 8 this IS C4, N=4096)
+
+Algorithmic bytes: topk / qsgd / ident 4*N*D + 4*D; randk 4*N*K + 4*D (device-RNG
+indices cost no bytes).  value = algorithmic bytes of all ranks / max-over-ranks step time.
+
+roofline: the dominant kernel's algorithmic bytes per launch / its mean launch time, timed with
+HIP events on its launch stream inside the timed region (flc_profile_*); peak 8.0 TB/s
+(MI355X_MICROARCH.md).  traffic: HBM bytes per launch from rocprofv3 PMC passes
+(profiles/pmc_<workload>.json, written by profiles/collect_pmc.py), or null.
+cpu_baseline: the oracle (numpy restatement of the reference path) timed on this host, rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
+
+WORKLOADS = {
+    "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2),
+    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_scatter", config=1),
+    "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ew_accum_vec", config=3),
+}
+
+
+def algorithmic_bytes(spec, n, d, k):
+    if spec.startswith("randk"):
+        return 4 * n * k + 4 * d
+    return 4 * n * d + 4 * d
+
+
+def kernel_bytes(kernel, n, d, k):
+    """Algorithmic bytes one launch of the dominant kernel must move."""
+    if kernel == "k_randk_scatter":
+        return 8 * n * k            # gather K values per row + write K (idx, value) entries
+    if kernel == "k_ew_accum_vec":
+        return 4 * n * d + 4 * d    # read every row once, write the [D] result
+    return 4 * n * d                # k_topk_filter: read every row once
+
+
+def cpu_baseline(spec, d, budget_s=12.0):
+    """Oracle (numpy, 1 core) encode + sequential reduce of a bounded sample of rows."""
+    from oracle import codecs as oc
+    from oracle.rng import OracleRandomState
+    g = np.random.default_rng(0)
+    rs = OracleRandomState(123)
+    t0 = time.perf_counter()
+    rows = 0
+    acc = None
+    while True:
+        x = g.standard_normal(d).astype(np.float32)
+        o = oc.OracleCompressor(spec, d)
+        o.generate(rs)
+        rs.randint31()
+        e = o.compress(x)
+        acc = e if acc is None else acc + e
+        rows += 1
+        if time.perf_counter() - t0 > budget_s or rows >= 64:
+            break
+    dt = time.perf_counter() - t0
+    k = math.ceil(0.01 * d)
+    return {"value": round(algorithmic_bytes(spec, rows, d, k) / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"oracle/codecs.py {spec}: pattern + encode + sequential fp32 reduce of {rows} rows x D={d} "
+                      f"({dt:.1f} s, numpy single-threaded)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
+    ap.add_argument("--d", type=int, default=None, help="override D")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    wl = dict(WORKLOADS[args.workload])
+    if args.n:
+        wl["n"] = args.n
+    if args.d:
+        wl["d"] = args.d
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from flpytorch_amd import _lib
+    from flpytorch_amd import aggregation as ag
+
+    n, d, spec = wl["n"], wl["d"], wl["spec"]
+    comp = ag.initCompressor(spec, d)
+    k = getattr(comp, "K", 0) or 0
+    # synthetic rows ~ N(0, 1) fp32, seeded per rank (device generator; never leaves HBM)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    rows = torch.empty((n, d), dtype=torch.float32, device=dev)
+    for i in range(0, n, 64):
+        rows[i:i + 64].normal_(generator=gen)
+    out = torch.empty(d, dtype=torch.float32, device=dev)
+    red = ag.UplinkReducer(comp, device=dev, seed=20241015)
+    client0 = rank * n
+
+    def step():
+        if world == 1:
+            red(rows, out=out, client0=client0)
+        else:
+            # local partial = sum_i C_i(row_i) in client order (fp32 divisor 1.0 keeps it exact),
+            # one RCCL sum over the ranks, then the global mean
+            red(rows, out=out, client0=client0, divisor=1.0)
+            dist.all_reduce(out)
+            out.div_(float(n * world))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _lib.profile_enable(True)
+    _lib.profile_collect(wl["kernel"])          # drop anything recorded before the timed region
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    kms, klaunch = _lib.profile_collect(wl["kernel"])
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    step_ms = elapsed / args.steps * 1e3
+    total_bytes = algorithmic_bytes(spec, n, d, k) * world
+    value = total_bytes / (elapsed / args.steps) / 1e9
+    kb = kernel_bytes(wl["kernel"], n, d, k)
+    kavg_ms = kms / max(klaunch, 1)
+    achieved = kb / (kavg_ms * 1e-3) / 1e9 if klaunch else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d)
+        line = {
+            "metric": "gradient-codec encode+reduce GB/s (device-resident), [N,D] fp32; % HBM peak",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic N(0,1) fp32 rows generated on device (seeded per rank); device-RNG patterns",
+            "config": {"workload": f"C{wl['config'] + 1} {spec} N={n}/GPU D={d}", "codec": spec,
+                       "clients_per_gpu": n, "clients_total": n * world, "D": d, "K": k,
+                       "parallelism": f"client-shard dp{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+            "pct_hbm_peak": round(100.0 * value / world / PEAK_GBS, 2),
+            "roofline": {"bound": "hbm", "kernel": wl["kernel"],
+                         "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+                         "bytes_per_launch": kb, "avg_launch_ms": round(kavg_ms, 4), "launches": klaunch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+"""ctypes binding of libflcodec.so (the C ABI in include/flcodec.h).
+
+The library is the product: there is no CPU fallback.  If the shared object is missing, or no
+MI355X is visible when a compute entry point is called, the call raises — it never reroutes to
+anything else.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libflcodec.so")
+
+FLC_OK, FLC_ERR_ARG, FLC_ERR_DTYPE, FLC_ERR_HIP, FLC_ERR_WORKSPACE, FLC_ERR_UNSUPPORTED = range(6)
+FLC_IDENT, FLC_LAZY, FLC_RANDK, FLC_NATURAL, FLC_STD_DITHERING, FLC_NAT_DITHERING, FLC_TOPK = range(1, 8)
+FLC_NORM_LINF, FLC_NORM_L1, FLC_NORM_L2 = 0, 1, 2
+FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
+
+# every symbol include/flcodec.h declares (tests/test_abi.py checks the .so exports all of them)
+EXPORTS = [
+    "flc_version", "flc_last_error_string",
+    "flc_reduce_rows", "flc_reduce_matrix",
+    "flc_encode_workspace_size", "flc_encode",
+    "flc_encode_reduce_workspace_size", "flc_encode_reduce",
+    "flc_mt_choice", "flc_mt_rand", "flc_mt_randint31",
+    "flc_device_uniform", "flc_device_randk_indices",
+    "flc_profile_enable", "flc_profile_collect",
+]
+
+
+class FlcCodecParams(ctypes.Structure):
+    _fields_ = [
+        ("codec", ctypes.c_int32),
+        ("s", ctypes.c_int32),
+        ("norm", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("k", ctypes.c_int64),
+        ("lazy_p", ctypes.c_float),
+        ("randk_scale", ctypes.c_float),
+        ("d_levels", ctypes.c_void_p),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class FlcPattern(ctypes.Structure):
+    _fields_ = [
+        ("d_randk_idx", ctypes.c_void_p),
+        ("d_uniforms", ctypes.c_void_p),
+        ("d_lazy_u", ctypes.c_void_p),
+        ("client0", ctypes.c_int64),
+        ("uniforms_ld", ctypes.c_int64),
+        ("idx_ld", ctypes.c_int64),
+    ]
+
+
+class FlcError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libflcodec.so (raises if it was not built — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"flpytorch_amd: {LIB_PATH} is missing — build it with "
+                "`make -C flpytorch_amd/csrc` (or __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, i64, f32, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_int, ctypes.c_size_t
+        P = ctypes.POINTER
+        lib.flc_version.restype = i32
+        lib.flc_last_error_string.restype = ctypes.c_char_p
+        lib.flc_reduce_rows.argtypes = [vp, i64, i64, vp, vp, f32, i32, vp, vp]
+        lib.flc_reduce_matrix.argtypes = [vp, i64, i64, i64, vp, vp, f32, i32, vp, vp]
+        lib.flc_encode_workspace_size.argtypes = [P(FlcCodecParams), i64]
+        lib.flc_encode_workspace_size.restype = sz
+        lib.flc_encode.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, vp, vp, vp, sz, vp]
+        lib.flc_encode_reduce_workspace_size.argtypes = [P(FlcCodecParams), i64, i64]
+        lib.flc_encode_reduce_workspace_size.restype = sz
+        lib.flc_encode_reduce.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, i64, i64, vp, f32, vp, vp,
+                                          vp, sz, vp]
+        lib.flc_mt_choice.argtypes = [vp, vp, i64, i64, vp, vp]
+        lib.flc_mt_rand.argtypes = [vp, vp, i64, vp]
+        lib.flc_mt_randint31.argtypes = [vp, vp, i64, vp]
+        lib.flc_device_uniform.argtypes = [ctypes.c_uint64, i64, i64]
+        lib.flc_device_uniform.restype = ctypes.c_double
+        lib.flc_device_randk_indices.argtypes = [ctypes.c_uint64, i64, i64, i64, vp]
+        lib.flc_profile_enable.argtypes = [i32]
+        lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
+        for name in EXPORTS:
+            if name not in ("flc_version", "flc_last_error_string", "flc_device_uniform",
+                            "flc_encode_workspace_size", "flc_encode_reduce_workspace_size"):
+                getattr(lib, name).restype = i32
+        _lib = lib
+        return lib
+
+
+def check(rc, what):
+    if rc == FLC_OK:
+        return
+    msg = f"{what}: {load().flc_last_error_string().decode(errors='replace')} (status {rc})"
+    if rc == FLC_ERR_ARG:
+        raise ValueError(msg)
+    if rc == FLC_ERR_DTYPE:
+        raise TypeError(msg)
+    if rc == FLC_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise FlcError(msg)
+
+
+def profile_enable(on=True):
+    load().flc_profile_enable(1 if on else 0)
+
+
+def profile_collect(kernel):
+    """(total_ms, launches) of one kernel name since the last collect (waits for its events)."""
+    ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+    check(load().flc_profile_collect(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)), "flc_profile_collect")
+    return ms.value, n.value
+
+
+def require_gpu():
+    """Raise unless an MI355X (HIP device) is visible — the product has no CPU path."""
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("flpytorch_amd: no HIP device visible — the codec/reduce path runs only on "
+                           "MI355X (gfx950); there is no CPU fallback")
+
+
+def stream_ptr(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Workspace:
+    """Per-device scratch for the library (grown on demand, reused across calls)."""
+
+    def __init__(self):
+        self._bufs = {}
+        self._lock = threading.Lock()
+
+    def get(self, device, nbytes):
+        import torch
+        key = (str(device), threading.get_ident())
+        with self._lock:
+            buf = self._bufs.get(key)
+            if buf is None or buf.numel() < nbytes:
+                buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+                self._bufs[key] = buf
+            return buf
+
+
+WORKSPACE = Workspace()

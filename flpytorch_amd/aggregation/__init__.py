@@ -1,0 +1,38 @@
+"""Drop-in aggregation plug-in: codecs + server reduction on MI355X.
+
+``install(compressors_module, algorithms_module)`` rebinds the reference's
+``utils.compressors.initCompressor`` / ``Compressor`` and the ``serverGradient`` of the algorithm
+classes whose reduction is the shared sequential fold (algorithms.py:1753-1768), so
+``fl_pytorch/run.py`` runs unchanged on top of libflcodec.
+"""
+from .compressors import (Compressor, CompressorType, initCompressor, stream_choice, stream_rand,  # noqa: F401
+                          stream_random, stream_randint31)
+from .fused import UplinkReducer  # noqa: F401
+from .reduce import (reduce_client_models, reduce_rows, serverGradientMaster,  # noqa: F401
+                     serverGradientPlain)
+
+# Algorithm classes whose serverGradient is exactly the shared fold, and what follows it.
+PLAIN_FOLD = ("FedAvg", "FedProx")                  # return gs            (1810-1832, 1886-1908)
+MASTER_FOLD = ("DCGD", "EF21")                      # master compressor    (1748-1770, 1521-1546)
+
+
+def install(compressors_module, algorithms_module=None):
+    """Rebind the reference's codec factory and reducers to the MI355X implementations.
+
+    Returns a callable that restores the originals."""
+    saved = [(compressors_module, "initCompressor", compressors_module.initCompressor),
+             (compressors_module, "Compressor", compressors_module.Compressor)]
+    compressors_module.initCompressor = initCompressor
+    compressors_module.Compressor = Compressor
+    if algorithms_module is not None:
+        for name, fn in [(n, serverGradientPlain) for n in PLAIN_FOLD] + [(n, serverGradientMaster) for n in MASTER_FOLD]:
+            cls = getattr(algorithms_module, name, None)
+            if cls is None:
+                continue
+            saved.append((cls, "serverGradient", cls.__dict__["serverGradient"]))
+            cls.serverGradient = staticmethod(fn)
+
+    def restore():
+        for obj, attr, val in reversed(saved):
+            setattr(obj, attr, val)
+    return restore

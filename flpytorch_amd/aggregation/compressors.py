@@ -1,0 +1,390 @@
+"""Drop-in ``Compressor`` for FL_PyTorch's codec protocol, executed on MI355X.
+
+Mirrors the object protocol of ``fl_pytorch/utils/compressors.py`` — the factory
+``initCompressor(spec, D)`` (435-494), the ``make*`` constructors and constants (64-194),
+``generateCompressPattern(rndgen, device, clientId, H)`` (196-216), ``compressVector(x)``
+(218-371) and the wire-size statistics (25-38, 223-224, 367-368) — so the reference's algorithm
+classes and ``run.py`` drive it unchanged (see ``flpytorch_amd.aggregation.install``).
+
+Where the work runs
+-------------------
+* Patterns (compat mode, the default) are drawn from the caller's own ``np.random.RandomState``
+  by libflcodec's host MT19937 (``flc_mt_*``): the state is read with ``get_state()``, advanced
+  in C++ exactly as numpy would advance it, and written back with ``set_state()`` — the shared
+  experiment stream stays bit-identical to the reference's.
+* Encoding always runs in the HIP kernels of libflcodec.so (``flc_encode``).  A host tensor is
+  copied to the GPU and the result copied back (the simulator's end-to-end path); with no HIP
+  device visible the call raises — there is no CPU implementation in the product.
+
+Error behaviour follows the reference: an unknown spec raises ``AssertionError`` (492); a
+non-fp32 input raises ``TypeError`` (the kernels are fp32-only).
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from .. import _lib
+
+
+class CompressorType:
+    """Same ids as the reference (compressors.py:11-19) and the C ABI's flc_codec."""
+    IDENTICAL = 1
+    LAZY_COMPRESSOR = 2
+    RANDK_COMPRESSOR = 3
+    NATURAL_COMPRESSOR_FP32 = 4
+    STANDARD_DITHERING_FP32 = 5
+    NATURAL_DITHERING_FP32 = 6
+    TOPK_COMPRESSOR = 7
+    RANK_K_COMPRESSOR = 8
+
+
+_OMEGA = r'$\omega$'
+
+
+# ---------------------------------------------------------------------------------------------
+# numpy legacy stream, advanced by libflcodec (bit-identical to RandomState's own draws)
+# ---------------------------------------------------------------------------------------------
+class _StreamState:
+    """Borrow a RandomState's MT19937 state for libflcodec; ``commit`` hands it back."""
+
+    def __init__(self, rndgen):
+        st = rndgen.get_state()
+        if st[0] != "MT19937":
+            raise TypeError("generateCompressPattern: rndgen must be a numpy RandomState (MT19937)")
+        self.rndgen = rndgen
+        self.key = np.array(st[1], dtype=np.uint32, copy=True)
+        self.pos = np.array([st[2]], dtype=np.int32)
+        self.gauss = (st[3], st[4])
+
+    def ptrs(self):
+        return ctypes.c_void_p(self.key.ctypes.data), ctypes.c_void_p(self.pos.ctypes.data)
+
+    def commit(self):
+        self.rndgen.set_state(("MT19937", self.key, int(self.pos[0]), self.gauss[0], self.gauss[1]))
+
+
+def stream_choice(rndgen, n, k):
+    """== rndgen.choice(n, k, replace=False) (numpy legacy), drawn by libflcodec."""
+    lib = _lib.load()
+    s = _StreamState(rndgen)
+    out = np.empty(k, dtype=np.int64)
+    scratch = np.empty(max(n, 1), dtype=np.int64)
+    _lib.check(lib.flc_mt_choice(*s.ptrs(), n, k, out.ctypes.data, scratch.ctypes.data), "flc_mt_choice")
+    s.commit()
+    return out
+
+
+def stream_rand(rndgen, n, out=None):
+    """== rndgen.rand(n) (float64), drawn by libflcodec into `out` (e.g. pinned host memory)."""
+    lib = _lib.load()
+    s = _StreamState(rndgen)
+    if out is None:
+        out = np.empty(n, dtype=np.float64)
+    _lib.check(lib.flc_mt_rand(*s.ptrs(), n, out.ctypes.data), "flc_mt_rand")
+    s.commit()
+    return out
+
+
+def stream_random(rndgen):
+    """== rndgen.random()."""
+    return float(stream_rand(rndgen, 1)[0])
+
+
+def stream_randint31(rndgen, count=1):
+    """== [rndgen.randint(2**31) for _ in range(count)]."""
+    lib = _lib.load()
+    s = _StreamState(rndgen)
+    out = np.empty(count, dtype=np.int64)
+    _lib.check(lib.flc_mt_randint31(*s.ptrs(), count, out.ctypes.data), "flc_mt_randint31")
+    s.commit()
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Level tables — built with the same torch calls as the reference so the fp32 values match
+# ---------------------------------------------------------------------------------------------
+def std_levels(levels):
+    return torch.arange(0.0, 1.0 + 1.0 / levels * 0.5, 1.0 / levels)          # compressors.py:87
+
+
+def nat_levels(levels):
+    v = torch.zeros(levels + 1)                                               # compressors.py:116-119
+    v[:levels] = torch.tensor([(1.0 / 2.0) ** i for i in range(levels)])
+    return torch.flip(v, dims=[0])
+
+
+def _gpu_device(x):
+    _lib.require_gpu()
+    if x.is_cuda:
+        return x.device
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class Compressor:
+    """Unbiased / contractive gradient codecs (E[C(x)] = x, E|C(x)-x|^2 <= w|x|^2, or top-K)."""
+
+    # -- statistics (compressors.py:25-38) -------------------------------------------------
+    def resetStats(self):
+        self.total_input_components = 0
+        self.really_need_to_send_components = 0
+        self.last_input_advance = 0
+        self.last_need_to_send_advance = 0
+
+    def __init__(self):
+        self.compressorType = CompressorType.IDENTICAL
+        self.resetStats()
+        self.device_rng = None   # (seed, client) -> device counter-based patterns (opt-in)
+
+    # -- constants -------------------------------------------------------------------------
+    def fullName(self):
+        t = self.compressorType
+        if t == CompressorType.IDENTICAL:
+            return "Identical"
+        if t == CompressorType.LAZY_COMPRESSOR:
+            return f"Bernoulli(Lazy) [p={self.P:g},{_OMEGA}={self.getW():.1f}]"
+        if t == CompressorType.RANDK_COMPRESSOR:
+            return f"Rand [K={self.K},D={self.D}]"
+        if t == CompressorType.NATURAL_COMPRESSOR_FP32:
+            return f"Natural for fp32 [{_OMEGA}={self.getW():.1f}]"
+        if t == CompressorType.STANDARD_DITHERING_FP32:
+            return f"Standard Dithering for fp32[s={self.s}]"
+        if t == CompressorType.NATURAL_DITHERING_FP32:
+            return f"Natural Dithering for fp32[s={self.s},{_OMEGA}={self.getW():.1f}]"
+        if t == CompressorType.TOPK_COMPRESSOR:
+            return f"Top [K={self.K},D={self.D}]"
+        if t == CompressorType.RANK_K_COMPRESSOR:
+            return f"Rank [K={self.K},D={self.D}]"
+        return "?"
+
+    def makeIdenticalCompressor(self):
+        self.compressorType = CompressorType.IDENTICAL
+        self.w = 0.0
+        self.resetStats()
+
+    def makeLazyCompressor(self, P):
+        self.compressorType = CompressorType.LAZY_COMPRESSOR
+        self.P = P
+        self.w = 1.0 / P - 1.0
+        self.resetStats()
+
+    def makeStandardDitheringFP32(self, D, levels, p=float("inf")):
+        self.D = D
+        self.compressorType = CompressorType.STANDARD_DITHERING_FP32
+        self.levelsValues = std_levels(levels)
+        self.s = len(self.levelsValues) - 1
+        assert self.s == levels
+        self.p = p
+        self.w = 0.0
+        self.resetStats()
+
+    def makeQSGD_FP32(self, D, levels):
+        self.makeStandardDitheringFP32(D, levels, p=2)
+        self.w = min(D / (levels * levels), D ** 0.5 / levels)   # QSGD Lemma 3.1
+
+    def makeTernGrad(self, D):
+        self.makeStandardDitheringFP32(D, levels=1, p=float("inf"))
+        self.w = 0.0
+
+    def makeNaturalDitheringFP32(self, D, levels, p=float("inf")):
+        self.D = D
+        self.compressorType = CompressorType.NATURAL_DITHERING_FP32
+        self.levelsValues = nat_levels(levels)
+        self.s = len(self.levelsValues) - 1
+        assert self.s == levels
+        self.p = p
+        r = min(p, 2)
+        self.w = 1.0 / 8.0 + (D ** (1.0 / r)) / (2 ** (self.s - 1)) * min(1, (D ** (1.0 / r)) / (2 ** (self.s - 1)))
+        self.resetStats()
+
+    def makeRandKCompressor(self, D, K):
+        self.compressorType = CompressorType.RANDK_COMPRESSOR
+        self.K = K
+        self.D = D
+        self.w = self.D / self.K - 1.0
+        self.resetStats()
+
+    def makeTopKCompressor(self, D, K):
+        self.compressorType = CompressorType.TOPK_COMPRESSOR
+        self.K = K
+        self.D = D
+        self.alpha = self.K / self.D
+        self.resetStats()
+
+    def makeRankKCompressor(self, D, K):
+        self.compressorType = CompressorType.RANK_K_COMPRESSOR
+        self.K = K
+        self.D = D
+        a = int(D ** 0.5)
+        while self.D % a != 0:
+            a += 1
+        self.A, self.B = a, self.D // a
+        self.alpha = self.K / min(self.A, self.B)
+        self.resetStats()
+
+    def makeNaturalCompressorFP32(self, D):
+        self.compressorType = CompressorType.NATURAL_COMPRESSOR_FP32
+        self.D = D
+        self.w = 1.0 / 8.0
+        self.resetStats()
+
+    def getW(self):
+        return self.w
+
+    def getAlphaContraction(self):
+        return self.alpha
+
+    def isContractionCompressor(self):
+        return hasattr(self, "alpha")
+
+    def isUnbiasedCompressor(self):
+        return hasattr(self, "w")
+
+    # -- patterns (compressors.py:196-216) ---------------------------------------------------
+    def generateCompressPattern(self, rndgen, device, clientId, H):
+        t = self.compressorType
+        if t == CompressorType.LAZY_COMPRESSOR:
+            self.testp = stream_random(rndgen)
+        elif t == CompressorType.RANDK_COMPRESSOR:
+            self.S = torch.from_numpy(stream_choice(rndgen, self.D, self.K)).to(torch.long).to(device=device)
+        elif t in (CompressorType.NATURAL_COMPRESSOR_FP32, CompressorType.STANDARD_DITHERING_FP32,
+                   CompressorType.NATURAL_DITHERING_FP32):
+            pin = torch.cuda.is_available()
+            buf = torch.empty(self.D, dtype=torch.float64, pin_memory=pin)
+            stream_rand(rndgen, self.D, out=buf.numpy())
+            self.testp = buf
+
+    # -- encode (compressors.py:218-371) -----------------------------------------------------
+    def codec_params(self, device):
+        """flc_codec_params for this compressor (levels uploaded to `device`)."""
+        t = self.compressorType
+        prm = _lib.FlcCodecParams()
+        prm.codec = int(t)
+        if t in (CompressorType.RANDK_COMPRESSOR, CompressorType.TOPK_COMPRESSOR):
+            prm.k = int(self.K)
+        if t == CompressorType.RANDK_COMPRESSOR:
+            prm.randk_scale = float(np.float32(self.D / self.K))
+        if t == CompressorType.LAZY_COMPRESSOR:
+            prm.lazy_p = float(np.float32(self.P))
+        keep = []
+        if t in (CompressorType.STANDARD_DITHERING_FP32, CompressorType.NATURAL_DITHERING_FP32):
+            if self.levelsValues.device != device:
+                self.levelsValues = self.levelsValues.to(device=device)
+            prm.s = int(self.s)
+            norms = {1: _lib.FLC_NORM_L1, 2: _lib.FLC_NORM_L2, math.inf: _lib.FLC_NORM_LINF}
+            if self.p not in norms:
+                raise NotImplementedError(f"p-norm {self.p}: flcodec implements p in (1, 2, inf)")
+            prm.norm = norms[self.p]
+            prm.d_levels = self.levelsValues.data_ptr()
+            keep.append(self.levelsValues)
+        if self.device_rng is not None:
+            prm.seed = int(self.device_rng[0]) & 0xFFFFFFFFFFFFFFFF
+        return prm, keep
+
+    def compressVector(self, x):
+        d = max(x.shape)
+        self.last_input_advance = d
+        self.last_need_to_send_advance = 0
+        t = self.compressorType
+        if t == CompressorType.IDENTICAL:
+            out = x                                                     # alias, like the reference
+            self.last_need_to_send_advance = d
+        elif t == CompressorType.RANK_K_COMPRESSOR:
+            raise NotImplementedError("rank_k (dense SVD, SURVEY §8f) is not in flcodec yet")
+        else:
+            out = self._encode_gpu(x)
+            if t == CompressorType.LAZY_COMPRESSOR:
+                self.last_need_to_send_advance = d if self.testp < self.P else 0
+            elif t in (CompressorType.RANDK_COMPRESSOR, CompressorType.TOPK_COMPRESSOR):
+                self.last_need_to_send_advance = self.K
+            elif t == CompressorType.NATURAL_COMPRESSOR_FP32:
+                self.last_need_to_send_advance = 9.0 / 32.0 * d
+            else:
+                self.last_need_to_send_advance = 1.0 + d * (1.0 + math.ceil(math.log2(self.s))) / 32.0
+        self.really_need_to_send_components += self.last_need_to_send_advance
+        self.total_input_components += self.last_input_advance
+        return out
+
+    def _encode_gpu(self, x, pnorm_in=None, pnorm_out=None):
+        if x.dtype != torch.float32:
+            raise TypeError(f"flcodec encodes fp32 only (got {x.dtype})")
+        dev = _gpu_device(x)
+        host_in = not x.is_cuda
+        xd = x.reshape(-1).to(device=dev).contiguous()
+        d = xd.numel()
+        t = self.compressorType
+        lib = _lib.load()
+        prm, keep = self.codec_params(dev)
+        pat = _lib.FlcPattern()
+        if self.device_rng is not None:
+            pat.client0 = int(self.device_rng[1])
+        if t == CompressorType.LAZY_COMPRESSOR:
+            u = torch.tensor([self.testp], dtype=torch.float64, device=dev)
+            pat.d_lazy_u = u.data_ptr()
+            keep.append(u)
+        elif t == CompressorType.RANDK_COMPRESSOR and self.device_rng is None:
+            if self.S.device != dev:
+                self.S = self.S.to(device=dev)
+            S = self.S.to(torch.int64).contiguous()
+            pat.d_randk_idx = S.data_ptr()
+            pat.idx_ld = S.numel()
+            keep.append(S)
+        elif t in (CompressorType.NATURAL_COMPRESSOR_FP32, CompressorType.STANDARD_DITHERING_FP32,
+                   CompressorType.NATURAL_DITHERING_FP32) and self.device_rng is None:
+            if self.testp.device != dev:
+                self.testp = self.testp.to(device=dev, non_blocking=True)
+            pat.d_uniforms = self.testp.data_ptr()
+        out = torch.empty_like(xd)
+        ws_bytes = lib.flc_encode_workspace_size(ctypes.byref(prm), d)
+        ws = _lib.WORKSPACE.get(dev, ws_bytes)
+        with torch.cuda.device(dev):
+            rc = lib.flc_encode(ctypes.byref(prm), ctypes.byref(pat), ctypes.c_void_p(xd.data_ptr()), d,
+                                ctypes.c_void_p(pnorm_in.data_ptr() if pnorm_in is not None else None),
+                                ctypes.c_void_p(pnorm_out.data_ptr() if pnorm_out is not None else None),
+                                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_encode")
+        out = out.reshape(x.shape)
+        return out.to("cpu") if host_in else out
+
+
+def initCompressor(compressorCmdLine, D):
+    """Spec grammar of compressors.py:435-494: name[:arg[:arg]], K as count or percent."""
+    params = compressorCmdLine.split(":")
+    name = params[0]
+    c = Compressor()
+
+    def count_or_percent(arg):
+        if arg.find("%") == -1:
+            return math.ceil(float(arg))
+        return math.ceil(float(arg[0:-1]) / 100.0 * D)
+
+    def pnorm_arg():
+        if len(params) == 3:
+            return math.inf if params[2].lower() == "inf" else int(params[2])
+        return math.inf
+
+    if name == "ident":
+        c.makeIdenticalCompressor()
+    elif name == "randk":
+        c.makeRandKCompressor(D, count_or_percent(params[1]))
+    elif name == "bernulli":
+        c.makeLazyCompressor(float(params[1]))
+    elif name == "natural":
+        c.makeNaturalCompressorFP32(D)
+    elif name == "qsgd":
+        c.makeQSGD_FP32(D, int(params[1]))
+    elif name == "nat.dithering":
+        c.makeNaturalDitheringFP32(D, int(params[1]), pnorm_arg())
+    elif name == "std.dithering":
+        c.makeStandardDitheringFP32(D, int(params[1]), pnorm_arg())
+    elif name == "topk":
+        c.makeTopKCompressor(D, count_or_percent(params[1]))
+    elif name == "rank_k":
+        c.makeRankKCompressor(D, count_or_percent(params[1]))
+    elif name == "terngrad":
+        c.makeTernGrad(D)
+    else:
+        raise AssertionError("Unknown compressor format")
+    return c

@@ -1,0 +1,109 @@
+"""Fused uplink of one round: encode every client row with its codec and reduce, one call.
+
+    out = (sum_i w_i * C_i(g_i)) / sum(w)        (flc_encode_reduce)
+
+``C_i`` is the compressor of client i (``compressors.py:218-371``) under its own pattern; the sum
+runs in client order with fp32 rounding per operation, i.e. bit-identical to encoding each row
+with ``compressVector`` and reducing the dense outputs sequentially (the reference's
+``serverGradient`` order, algorithms.py:1753-1768) — without materialising the N dense outputs.
+
+Pattern sources
+  * compat  — the reference's numpy stream: RandK index sets [N, K] int64 and dithering /
+              natural uniforms [N, D] float64 drawn on the host (``stream_choice`` /
+              ``stream_rand``) and uploaded; lazy draws [N] float64.
+  * device  — counter-based draws keyed by (seed, client id, element) generated inside the
+              kernels: no host work, no uniform bytes (the benchmark mode).
+"""
+import ctypes
+
+import torch
+
+from .. import _lib
+from .compressors import Compressor, CompressorType
+
+
+class UplinkReducer:
+    """Holds the codec constants + workspace for repeated fused encode+reduce calls."""
+
+    def __init__(self, compressor: Compressor, device=None, seed=None):
+        _lib.require_gpu()
+        self.comp = compressor
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.seed = seed
+        if compressor.compressorType == CompressorType.RANK_K_COMPRESSOR:
+            raise NotImplementedError("rank_k is not in flcodec yet (SURVEY §8f)")
+
+    def params(self):
+        prm, keep = self.comp.codec_params(self.device)
+        if self.seed is not None:
+            prm.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        return prm, keep
+
+    def workspace_bytes(self, n, d):
+        prm, _ = self.params()
+        return _lib.load().flc_encode_reduce_workspace_size(ctypes.byref(prm), n, d)
+
+    def __call__(self, rows, out=None, weights=None, client0=0, randk_idx=None, uniforms=None, lazy_u=None,
+                 pnorms_out=None, stream=None, divisor=None):
+        """rows: [N, D] fp32 device tensor (row stride % 4 == 0 for the vector path) or a list of
+        [D] device tensors.  Compat patterns: randk_idx [N, K] int64, uniforms [N, D] float64,
+        lazy_u [N] float64 (device).  Without them (and with ``seed`` set) draws are on device.
+        ``divisor`` overrides the fp32 divisor sum(w) (e.g. 1.0 for a partial sum across GPUs)."""
+        lib = _lib.load()
+        dev = self.device
+        prm, keep = self.params()
+        pat = _lib.FlcPattern()
+        pat.client0 = int(client0)
+        if torch.is_tensor(rows) and rows.dim() == 2:
+            n, d = rows.shape
+            base, ld, ptrs = rows.data_ptr(), rows.stride(0), None
+            if rows.stride(1) != 1:
+                raise ValueError("rows must be row-contiguous")
+        else:
+            n = len(rows)
+            d = rows[0].numel() if n else 0
+            # the pointer-array entry reads rows with 16-byte vector loads: keep them aligned
+            rows = [r if (r.is_contiguous() and r.data_ptr() % 16 == 0) else r.contiguous().clone() for r in rows]
+            keep.extend(rows)
+            pt = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+            keep.append(pt)
+            base, ld, ptrs = None, 0, pt.data_ptr()
+        if out is None:
+            out = torch.empty(d, dtype=torch.float32, device=dev)
+        t = self.comp.compressorType
+        if t == CompressorType.RANDK_COMPRESSOR and randk_idx is not None:
+            pat.d_randk_idx = randk_idx.data_ptr()
+            pat.idx_ld = randk_idx.stride(0)
+        if uniforms is not None:
+            pat.d_uniforms = uniforms.data_ptr()
+            pat.uniforms_ld = uniforms.stride(0)
+        if t == CompressorType.LAZY_COMPRESSOR:
+            if lazy_u is None:
+                raise ValueError("lazy codec needs lazy_u [N] draws")
+            pat.d_lazy_u = lazy_u.data_ptr()
+        needs_seed = (t in (CompressorType.RANDK_COMPRESSOR,) and randk_idx is None) or \
+                     (t in (CompressorType.NATURAL_COMPRESSOR_FP32, CompressorType.STANDARD_DITHERING_FP32)
+                      and uniforms is None)
+        if needs_seed and self.seed is None:
+            raise ValueError("no compat pattern given and no device-RNG seed set")
+        w_ptr, total = None, float(n)
+        if weights is not None:
+            weights = [float(w) for w in weights]
+            total = weights[0]
+            for w in weights[1:]:
+                total += w
+            wt = torch.tensor(weights, dtype=torch.float32, device=dev)
+            keep.append(wt)
+            w_ptr = wt.data_ptr()
+        if divisor is not None:
+            total = float(divisor)
+        ws_bytes = lib.flc_encode_reduce_workspace_size(ctypes.byref(prm), n, d)
+        ws = _lib.WORKSPACE.get(dev, ws_bytes)
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _lib.stream_ptr(dev)
+        with torch.cuda.device(dev):
+            rc = lib.flc_encode_reduce(ctypes.byref(prm), ctypes.byref(pat), ctypes.c_void_p(base), ld,
+                                       ctypes.c_void_p(ptrs), n, d, ctypes.c_void_p(w_ptr), ctypes.c_float(total),
+                                       ctypes.c_void_p(pnorms_out.data_ptr() if pnorms_out is not None else None),
+                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(), st)
+        _lib.check(rc, "flc_encode_reduce")
+        return out

@@ -1,0 +1,113 @@
+"""Server-side N-way reduction on MI355X — the ``serverGradient`` protocol.
+
+Reference: every compressed-gradient algorithm folds the client models the same way,
+``gs = w0 (x - x0); gs += wi (x - xi); gs / sum(w)`` in Buffer order
+(fl_pytorch/utils/algorithms.py: DCGD 1748-1770, FedAvg 1810-1832, FedProx 1886-1908,
+EF21 1521-1546, ...), then some return ``gs`` and the others pass it through the master
+compressor (identity).  Here the fold is one ``flc_reduce_rows`` launch over a device array of
+the client-model pointers — no stacking copy — bit-identical to the sequential torch loop.
+
+Protocol kept from the reference (algorithms.py:2094-2125 and the class methods):
+  * ``waitForItem()`` once per client before ``get(i)``; reads ``r['model']`` and
+    ``r['client_state']['weight']``;
+  * honours ``H['fl_dtype']`` and ``params_current.device`` (host tensors are moved to the GPU
+    and the result moved back: the simulator's end-to-end path);
+  * returns a new tensor the caller owns; 0 clients -> zeros.
+"""
+import ctypes
+
+import torch
+
+from .. import _lib
+
+
+def _weights_and_total(weights):
+    """Python-float weights as the reference uses them: each wi applied as fp32, the total summed
+    as a python float in Buffer order and applied as the fp32 divisor."""
+    total = weights[0]
+    for w in weights[1:]:
+        total += w
+    uniform = all(float(w) == 1.0 for w in weights)
+    return uniform, float(total)
+
+
+def reduce_rows(x, rows, weights=None, relative=True, out=None):
+    """out = (sum_i w_i * (x - rows_i)) / sum(w)   (relative=True, client models in)
+       out = (sum_i w_i * rows_i) / sum(w)         (relative=False, client updates in)
+
+    ``rows`` is a list of fp32 device tensors shaped like ``x`` (or a 2-D [N, D] tensor).
+    """
+    _lib.require_gpu()
+    lib = _lib.load()
+    dev = x.device
+    n = rows.shape[0] if torch.is_tensor(rows) else len(rows)
+    d = x.numel()
+    if out is None:
+        out = torch.empty_like(x)
+    if n == 0:
+        return out.zero_()
+    weights = [1.0] * n if weights is None else [float(w) for w in weights]
+    uniform, total = _weights_and_total(weights)
+    keep = []
+    w_ptr = None
+    if not uniform:
+        wt = torch.tensor(weights, dtype=torch.float32, device=dev)
+        keep.append(wt)
+        w_ptr = wt.data_ptr()
+    x_ptr = x.data_ptr() if relative else None
+    mode = _lib.FLC_REDUCE_REL_X if relative else _lib.FLC_REDUCE_PLAIN
+    with torch.cuda.device(dev):
+        if torch.is_tensor(rows) and rows.dim() == 2:
+            rc = lib.flc_reduce_matrix(ctypes.c_void_p(rows.data_ptr()), rows.stride(0), n, d,
+                                       ctypes.c_void_p(x_ptr), ctypes.c_void_p(w_ptr), ctypes.c_float(total), mode,
+                                       ctypes.c_void_p(out.data_ptr()), _lib.stream_ptr(dev))
+        else:
+            rows = [r if (r.data_ptr() % 16 == 0 and r.is_contiguous()) else r.contiguous().clone() for r in rows]
+            ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+            keep.append(ptrs)
+            rc = lib.flc_reduce_rows(ctypes.c_void_p(ptrs.data_ptr()), n, d, ctypes.c_void_p(x_ptr),
+                                     ctypes.c_void_p(w_ptr), ctypes.c_float(total), mode,
+                                     ctypes.c_void_p(out.data_ptr()), _lib.stream_ptr(dev))
+    _lib.check(rc, "flc_reduce")
+    return out
+
+
+def reduce_client_models(clients_responses, clients, params_current, H):
+    """The shared core of the reference's serverGradient bodies (algorithms.py:1753-1768)."""
+    if clients == 0:
+        return torch.zeros_like(params_current)                  # algorithms.py:2117-2118
+    fl_dtype = H["fl_dtype"]
+    if fl_dtype != torch.float32 or params_current.dtype != torch.float32:
+        raise TypeError(f"flcodec reduces fp32 only (fl_dtype={fl_dtype})")
+    _lib.require_gpu()
+    host = not params_current.is_cuda
+    dev = params_current.device if not host else torch.device("cuda", torch.cuda.current_device())
+    models, weights = [], []
+    for i in range(clients):
+        clients_responses.waitForItem()
+        r = clients_responses.get(i)
+        models.append(r["model"].to(device=dev, dtype=fl_dtype).reshape(-1))
+        weights.append(r["client_state"]["weight"])
+    x = params_current.to(device=dev).reshape(-1).contiguous()
+    gs = reduce_rows(x, models, weights, relative=True)
+    gs = gs.reshape(params_current.shape)
+    return gs.to(params_current.device) if host else gs
+
+
+def make_server_gradient(master_compress):
+    """A ``serverGradient`` static method body: plain (FedAvg, FedProx) or followed by
+    ``H['compressor_master'].compressVector`` (DCGD, EF21)."""
+
+    def serverGradient(clients_responses, clients, model, params_current, H):
+        gs = reduce_client_models(clients_responses, clients, params_current, H)
+        if master_compress:
+            return H["compressor_master"].compressVector(gs)
+        return gs
+
+    serverGradient.__doc__ = ("serverGradient on MI355X (flcodec reduce)" +
+                              (" + master compressor" if master_compress else ""))
+    return serverGradient
+
+
+serverGradientPlain = make_server_gradient(False)
+serverGradientMaster = make_server_gradient(True)

@@ -1,0 +1,162 @@
+// C ABI entry points of libflcodec.so (declared in include/flcodec.h): argument checking,
+// workspace sizing and dispatch to the codec families.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace flc {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return FLC_ERR_HIP;
+}
+
+// ---- kernel timing ------------------------------------------------------------------------
+bool g_prof_on = false;
+namespace {
+std::mutex g_prof_mu;
+std::vector<hipEvent_t> g_ev_free;
+std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> g_prof;
+std::map<std::string, hipEvent_t> g_open;
+hipEvent_t take_event() {
+    if (!g_ev_free.empty()) { hipEvent_t e = g_ev_free.back(); g_ev_free.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+}  // namespace
+
+void prof_record(const char* name, hipStream_t st, bool begin) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    hipEvent_t e = take_event();
+    if (!e) return;
+    (void)hipEventRecord(e, st);
+    if (begin) {
+        g_open[name] = e;
+    } else {
+        auto it = g_open.find(name);
+        if (it == g_open.end()) { g_ev_free.push_back(e); return; }
+        g_prof[name].emplace_back(it->second, e);
+        g_open.erase(it);
+    }
+}
+
+static bool is_sel(int codec) { return codec == FLC_TOPK || codec == FLC_RANDK; }
+static bool known(int codec) { return codec >= FLC_IDENT && codec <= FLC_TOPK; }
+
+}  // namespace flc
+
+using namespace flc;
+
+extern "C" int flc_version(void) { return 100; }
+
+extern "C" int flc_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+    return FLC_OK;
+}
+
+extern "C" int flc_profile_collect(const char* kernel, double* h_total_ms, int64_t* h_launches) {
+    if (!kernel || !h_total_ms || !h_launches) { set_error("flc_profile_collect: null argument"); return FLC_ERR_ARG; }
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> recs;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        auto it = g_prof.find(kernel);
+        if (it != g_prof.end()) { recs.swap(it->second); g_prof.erase(it); }
+    }
+    double total = 0.0;
+    for (auto& r : recs) {
+        FLC_CHECK_HIP(hipEventSynchronize(r.second));
+        float ms = 0.f;
+        FLC_CHECK_HIP(hipEventElapsedTime(&ms, r.first, r.second));
+        total += ms;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        for (auto& r : recs) { g_ev_free.push_back(r.first); g_ev_free.push_back(r.second); }
+    }
+    *h_total_ms = total;
+    *h_launches = (int64_t)recs.size();
+    return FLC_OK;
+}
+
+extern "C" const char* flc_last_error_string(void) { return g_err; }
+
+extern "C" size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t d) {
+    if (!prm || !known(prm->codec)) return 0;
+    if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
+    if (prm->codec == FLC_RANDK) return 0;
+    return ew_workspace(prm, 1, d);
+}
+
+extern "C" size_t flc_encode_reduce_workspace_size(const flc_codec_params* prm, int64_t n, int64_t d) {
+    if (!prm || !known(prm->codec)) return 0;
+    if (is_sel(prm->codec)) return sel_workspace(prm, n, d);
+    return ew_workspace(prm, n, d);
+}
+
+extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+                          const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes,
+                          void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_encode: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (d < 0 || (d > 0 && (!d_x || !d_out))) { set_error("flc_encode: bad x/out/d"); return FLC_ERR_ARG; }
+    hipStream_t st = (hipStream_t)stream;
+    const bool vec = (((uintptr_t)d_x | (uintptr_t)d_out) & 15u) == 0;
+    switch (prm->codec) {
+        case FLC_RANDK:
+            if (!(pat && pat->d_randk_idx) && prm->k > d) { set_error("randk: K > D"); return FLC_ERR_ARG; }
+            return randk_dense(prm, pat, d_x, d, d_out, st);
+        case FLC_TOPK: {
+            RowSrc r{d_x, d, nullptr};
+            return sel_run(prm, pat, r, vec, 1, d, /*assign=*/true, nullptr, 1.f, d_out, d_ws, ws_bytes, st);
+        }
+        default: {
+            RowSrc s{d_x, d, nullptr};
+            return ew_run(prm, pat, s, vec, 1, d, d_pnorm_in, d_pnorm_out, /*dense=*/true, d_out, nullptr, 1.f, d_ws,
+                          ws_bytes, st);
+        }
+    }
+}
+
+extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern* pat, const float* d_rows, int64_t ld,
+                                 const float* const* d_row_ptrs, int64_t n, int64_t d, const float* d_w, float w_total,
+                                 float* d_pnorms_out, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_encode_reduce: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (n < 0 || d < 0 || (d > 0 && !d_out)) { set_error("flc_encode_reduce: bad n/d/out"); return FLC_ERR_ARG; }
+    if (n > 0 && d > 0 && !d_rows && !d_row_ptrs) { set_error("flc_encode_reduce: no rows"); return FLC_ERR_ARG; }
+    if (d_rows && ld < d) { set_error("flc_encode_reduce: ld < d"); return FLC_ERR_ARG; }
+    hipStream_t st = (hipStream_t)stream;
+    if (d == 0) return FLC_OK;
+    if (n == 0) {
+        FLC_CHECK_HIP(hipMemsetAsync(d_out, 0, (size_t)d * sizeof(float), st));
+        return FLC_OK;
+    }
+    // vector path: matrix rows 16-byte aligned with ld % 4 == 0; pointer rows are required aligned
+    const bool vec = d_rows ? ((((uintptr_t)d_rows & 15u) == 0) && (ld % 4 == 0)) : true;
+    if (prm->codec == FLC_IDENT) {
+        RowSrc s{d_rows, ld, d_row_ptrs};
+        return reduce_impl(s, vec, n, d, nullptr, d_w, w_total, FLC_REDUCE_PLAIN, d_out, st);
+    }
+    if (is_sel(prm->codec)) {
+        RowSrc r{d_rows, ld, d_row_ptrs};
+        return sel_run(prm, pat, r, vec, n, d, false, d_w, w_total, d_out, d_ws, ws_bytes, st);
+    }
+    RowSrc s{d_rows, ld, d_row_ptrs};
+    return ew_run(prm, pat, s, vec, n, d, nullptr, d_pnorms_out, false, d_out, d_w, w_total, d_ws, ws_bytes, st);
+}

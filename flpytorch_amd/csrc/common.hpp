@@ -1,0 +1,153 @@
+// Device/host helpers shared by the flcodec translation units (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/flcodec.h"
+
+namespace flc {
+
+constexpr int WAVE = 64;          // CDNA wavefront
+constexpr int CHUNK = 4096;       // elements per selection chunk (one wave's tile, 16 KB fp32)
+constexpr int CHUNK_SHIFT = 12;
+
+// ------------------------------------------------------------------------------------------
+// error plumbing (thread-local message, status codes of flcodec.h)
+// ------------------------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+
+#define FLC_CHECK_HIP(expr)                                          \
+    do {                                                             \
+        hipError_t _e = (expr);                                      \
+        if (_e != hipSuccess) return ::flc::hip_fail(_e, #expr);     \
+    } while (0)
+#define FLC_CHECK_LAUNCH(what)                                       \
+    do {                                                             \
+        hipError_t _e = hipGetLastError();                           \
+        if (_e != hipSuccess) return ::flc::hip_fail(_e, what);      \
+    } while (0)
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Kernel timing (flc_profile_enable): a scope records a hipEvent pair around one launch.
+extern bool g_prof_on;
+void prof_record(const char* name, hipStream_t st, bool begin);
+struct ProfScope {
+    const char* name;
+    hipStream_t st;
+    ProfScope(const char* n, hipStream_t s) : name(n), st(s) { if (g_prof_on) prof_record(name, st, true); }
+    ~ProfScope() { if (g_prof_on) prof_record(name, st, false); }
+};
+
+// Workspace carving: every sub-buffer 256-byte aligned.
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+    template <class T>
+    T* take(size_t count) {
+        off = align_up(off, 256);
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += count * sizeof(T);
+        return p;
+    }
+    size_t bytes() const { return align_up(off, 256); }
+};
+
+// Row addressing shared by every kernel: a strided matrix (row i at base + i*ld) or a device
+// array of row pointers (base == nullptr).
+struct RowSrc {
+    const float* base;
+    int64_t ld;
+    const float* const* ptrs;
+    __device__ inline const float* row(int64_t i) const { return base ? base + i * ld : ptrs[i]; }
+};
+
+// Internal entry points of the codec families (reduce.hip, codecs.hip, select.hip).
+int reduce_impl(RowSrc src, bool rows_vec_ok, int64_t n, int64_t d, const float* x, const float* w, float wt,
+                int mode, float* out, hipStream_t st);
+size_t ew_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool vec, int64_t n, int64_t d,
+           const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt, void* ws,
+           size_t ws_bytes, hipStream_t st);
+size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
+            bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st);
+int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out,
+                hipStream_t st);
+
+// ------------------------------------------------------------------------------------------
+// Device-RNG mode: counter-based generator, SplitMix64 finaliser over a keyed Weyl sequence.
+// uniform(seed, client, j) = (mix(seed, client, j) >> 11) * 2^-53 — a 53-bit double like
+// numpy's random_sample, so compat and device modes share every downstream comparison.
+// ------------------------------------------------------------------------------------------
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+__host__ __device__ inline uint64_t client_key(uint64_t seed, int64_t client) {
+    return mix64(seed ^ mix64(0x9E3779B97F4A7C15ull * (uint64_t)(client + 1)));
+}
+__host__ __device__ inline double uniform53(uint64_t ckey, int64_t j) {
+    uint64_t z = mix64(ckey + 0x9E3779B97F4A7C15ull * (uint64_t)j);
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Keyed bijection on [0, d): balanced Feistel on 2h bits (4^h >= d) with cycle walking.
+// RandK device mode takes the first K images: K distinct indices drawn uniformly.
+struct Feistel {
+    uint64_t key;
+    uint32_t half_bits;
+    uint32_t half_mask;
+    uint64_t d;
+    __host__ __device__ Feistel(uint64_t ckey, uint64_t dd) : key(ckey), d(dd) {
+        uint32_t b = 1;
+        while ((1ull << (2 * b)) < dd) ++b;
+        half_bits = b;
+        half_mask = (b >= 32) ? 0xFFFFFFFFu : ((1u << b) - 1u);
+    }
+    __host__ __device__ inline uint32_t round_fn(uint32_t r, int i) const {
+        return (uint32_t)mix64(key + ((uint64_t)i << 56) + r) & half_mask;
+    }
+    __host__ __device__ inline uint64_t once(uint64_t v) const {
+        uint32_t l = (uint32_t)(v >> half_bits) & half_mask, r = (uint32_t)v & half_mask;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t nl = r, nr = l ^ round_fn(r, i);
+            l = nl;
+            r = nr;
+        }
+        return ((uint64_t)l << half_bits) | r;
+    }
+    __host__ __device__ inline uint64_t operator()(uint64_t t) const {
+        uint64_t v = once(t);
+        while (v >= d) v = once(v);   // cycle walking stays inside [0, d)
+        return v;
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// Wave helpers
+// ------------------------------------------------------------------------------------------
+__device__ inline int lane_id() { return __lane_id(); }
+
+template <class T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+
+// |x| ordering key for TopK: sign cleared; NaN (0x7F8..1-0x7FF..F) above +inf, like torch.topk.
+__device__ inline uint32_t mag_key(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
+
+// torch.sign semantics: -1 / 0 / +1 (NaN -> 0 is irrelevant: a NaN row's norm is NaN).
+__device__ inline float tsign(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+}  // namespace flc

@@ -1,0 +1,678 @@
+// Sparsifying codecs: TopK (compressors.py:330-335) and RandK (240-245), dense single-vector
+// encode and fused batch encode + reduce.
+//
+// Data flow of the batch path (N client rows x D, chunk = 4096 elements = one wave's tile):
+//
+//   TopK  sample   : one workgroup per row keys a spread sample (<= 16 K elements, LDS) and picks a
+//                    conservative threshold T_lo with count(|x| >= T_lo) >= K w.h.p.
+//         filter   : ONE pass over every row (the only full HBM read): entries with key >= T_lo
+//                    are appended to the row's candidate list (idx, val), per chunk -> tab[c][row]
+//         select   : exact K-th largest key among the candidates (3 radix passes, 11/11/9 bits)
+//         fallback : rows whose list overflowed, came up short (sample unlucky), or whose K-th
+//                    magnitude is tied ambiguously are redone exactly on the full row
+//                    (3 radix passes + tie prefix + exact filter, ties -> lowest index first)
+//   RandK lists    : per row the K indices (numpy stream, or the device Feistel sampler) are
+//                    bucketed by chunk (count, scan, scatter) with value (D/K)*x[j]
+//   accumulate     : one wave owns one chunk as an fp32 LDS tile and folds the rows' admitted
+//                    entries in row order -> (sum_i w_i C_i(x_i)) / w_total, bit-identical to the
+//                    sequential reduction of the dense compressVector outputs (indices are
+//                    distinct within a row, so every element sees its terms in row order).
+//
+// Keys: |x| bits with the sign cleared (uint32, monotone; NaN above inf like torch.topk).
+#include "common.hpp"
+
+namespace flc {
+
+constexpr uint32_t ALL = 0xFFFFFFFFu;
+constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
+constexpr int SMAX = 16384;          // sample size kept in LDS
+constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
+
+struct SelWs {            // carved from the caller workspace
+    uint2* tab;           // [C][N] (offset, count) of each row's entries in chunk c
+    uint32_t* ent_idx;    // [N][cap] element index within the row
+    float* ent_val;       // [N][cap] entry value (already scaled for RandK)
+    uint32_t* rowcnt;     // [N] entries used
+    uint32_t* flags;      // [N]
+    uint32_t* thr;        // [N] admission key: entries with key >= thr are summed
+    uint32_t* prefix;     // [N] radix-select state
+    uint32_t* krem;       // [N]
+    uint32_t* tieprefix;  // [C][N] ties (key == thr) in chunks before c   (fallback only)
+    uint32_t* hist;       // [N][HBINS]
+    uint32_t* worklist;   // [N] rows on the exact path
+    uint32_t* nwork;      // [1]
+    uint32_t* cursor;     // [C][N] RandK scatter cursors
+    int64_t cap;
+};
+
+__device__ inline int64_t nchunks(int64_t d) { return (d + CHUNK - 1) >> CHUNK_SHIFT; }
+
+// ------------------------------------------------------------------------------------------
+// Block-level helpers
+// ------------------------------------------------------------------------------------------
+// Find, scanning a 2048-bin histogram from the TOP bin down, the bin b where the running count
+// reaches k (1-based).  Returns b and the count strictly above b.  256 threads, 8 bins each.
+__device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
+                                 uint32_t* scratch /* LDS 256+2 */) {
+    const int t = threadIdx.x;
+    // thread t owns bins [HBINS-8(t+1), HBINS-8t)  (top bins first)
+    uint32_t local[8];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { local[q] = h[HBINS - 1 - (t * 8 + q)]; s += local[q]; }
+    scratch[t] = s;
+    __syncthreads();
+    // inclusive scan (Hillis-Steele) over 256 thread sums
+    for (int off = 1; off < 256; off <<= 1) {
+        uint32_t v = (t >= off) ? scratch[t - off] : 0u;
+        __syncthreads();
+        scratch[t] += v;
+        __syncthreads();
+    }
+    uint32_t incl = scratch[t], excl = incl - s;
+    if (excl < k && incl >= k) {
+        uint32_t run = excl;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (run + local[q] >= k) {
+                scratch[256] = (uint32_t)(HBINS - 1 - (t * 8 + q));
+                scratch[257] = run;
+                break;
+            }
+            run += local[q];
+        }
+    }
+    __syncthreads();
+    bin = scratch[256];
+    above = scratch[257];
+    __syncthreads();
+}
+
+// pass p: 0 -> bits [30:20], 1 -> [19:9], 2 -> [8:0]
+__device__ inline uint32_t pass_shift(int p) { return p == 0 ? 20u : (p == 1 ? 9u : 0u); }
+__device__ inline uint32_t pass_bits(int p) { return p == 2 ? 9u : 11u; }
+__device__ inline bool key_in_prefix(uint32_t key, int p, uint32_t prefix) {
+    // prefix holds the bits above this pass's field
+    if (p == 0) return true;
+    uint32_t sh = pass_shift(p) + pass_bits(p);
+    return (key >> sh) == prefix;
+}
+__device__ inline uint32_t key_bin(uint32_t key, int p) {
+    return (key >> pass_shift(p)) & ((1u << pass_bits(p)) - 1u);
+}
+
+// ------------------------------------------------------------------------------------------
+// TopK: sample threshold (one workgroup per row)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws) {
+    __shared__ uint32_t keys[SMAX];
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    const int64_t row = blockIdx.x;
+    if (row >= n) return;
+    const float* r = rows.row(row);
+    // sample: the whole row if it fits, else P pieces of 256 contiguous elements spread evenly
+    int S;
+    if (d <= SMAX) {
+        S = (int)d;
+        for (int i = threadIdx.x; i < S; i += 256) keys[i] = mag_key(r[i]);
+    } else {
+        const int P = SMAX / 256;
+        S = SMAX;
+        for (int i = threadIdx.x; i < S; i += 256) {
+            int p = i >> 8, q = i & 255;
+            int64_t off = ((int64_t)p * (d - 256)) / (P - 1);
+            keys[i] = mag_key(r[off + q]);
+        }
+    }
+    // rank (from the top) of the sample element whose key is the threshold
+    uint32_t rank;
+    if (S == d) {
+        rank = (uint32_t)K;                                   // exact
+    } else {
+        double ks = (double)K * (double)S / (double)d;
+        double rr = ks + 4.0 * sqrt(ks) + 8.0;
+        rank = (uint32_t)min((double)S, ceil(rr));
+    }
+    uint32_t prefix = 0, krem = rank;
+    for (int p = 0; p < 3; ++p) {
+        for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < S; i += 256) {
+            uint32_t k = keys[i];
+            if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
+        }
+        __syncthreads();
+        uint32_t bin, above;
+        hist_find(h, krem, bin, above, scratch);
+        prefix = (prefix << pass_bits(p)) | bin;
+        krem -= above;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ws.thr[row] = (rank >= (uint32_t)S && S != d) ? 0u : prefix;
+        ws.flags[row] = 0;
+        ws.rowcnt[row] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Filter: append entries with key >= thr (fast path) or the exact selection (exact path).
+// One wave per chunk; a workgroup takes 4 chunks of one row; grid-stride over (row, 4-chunk).
+// Exact mode (rows on the worklist, F_EXACT): key > thr always; key == thr only while the
+// tie rank (tieprefix + rank in index order inside the chunk) < krem.
+// ------------------------------------------------------------------------------------------
+template <bool EXACT, bool VEC>
+__global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
+    const int64_t C = nchunks(d);
+    const int64_t bpr = (C + 3) / 4;                   // 4-chunk blocks per row
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nrows = EXACT ? (int64_t)(*ws.nwork) : n;
+    const int64_t items = nrows * bpr;
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int64_t li = it / bpr;
+        const int64_t row = EXACT ? (int64_t)ws.worklist[li] : li;
+        const int64_t c = (it % bpr) * 4 + wv;
+        if (!EXACT && ws.flags[row]) continue;          // already failed (row-uniform)
+        if (c >= C) continue;
+        const float* r = rows.row(row);
+        const int64_t j0 = c * CHUNK;
+        const uint32_t T = ws.thr[row];
+        // load the chunk: 16 x float4 per lane, element j0 + (t*64 + lane)*4 + q
+        float v[16][4];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int64_t j = j0 + (int64_t)(t * 64 + lane) * 4;
+            if (VEC && j + 3 < d) {
+                float4 f = *reinterpret_cast<const float4*>(r + j);
+                v[t][0] = f.x; v[t][1] = f.y; v[t][2] = f.z; v[t][3] = f.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[t][q] = (j + q < d) ? r[j + q] : 0.f;
+            }
+        }
+        uint32_t tie_base = 0, tie_need = ALL;
+        if (EXACT) { tie_base = ws.tieprefix[c * n + row]; tie_need = ws.krem[row]; }
+        // pass 1: count
+        uint32_t cnt = 0;
+        uint32_t tie_run = tie_base;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int64_t jb = j0 + (int64_t)(t * 64 + lane) * 4;
+            bool gt[4], eq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t k = mag_key(v[t][q]);
+                const bool inb = (jb + q) < d;
+                gt[q] = inb && (EXACT ? k > T : k >= T);
+                eq[q] = inb && EXACT && k == T;
+            }
+            if (EXACT) {
+                uint64_t m[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m[q] = __ballot(eq[q]);
+                const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                uint32_t before = __popcll(m[0] & lt) + __popcll(m[1] & lt) + __popcll(m[2] & lt) + __popcll(m[3] & lt);
+                uint32_t inlane = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (eq[q]) gt[q] = (tie_run + before + inlane) < tie_need;
+                    inlane += eq[q] ? 1u : 0u;
+                }
+                tie_run += __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cnt += gt[q] ? 1u : 0u;
+        }
+        cnt = wave_sum(cnt);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&ws.rowcnt[row], cnt);
+        base = __shfl(base, 0, WAVE);
+        const bool fits = (int64_t)base + cnt <= ws.cap;
+        if (lane == 0) {
+            ws.tab[c * n + row] = make_uint2(base, fits ? cnt : 0u);
+            if (!fits) atomicOr(&ws.flags[row], F_OVERFLOW);
+        }
+        if (!fits || cnt == 0) continue;
+        // pass 2: write (order inside the chunk is irrelevant to the result)
+        uint32_t run = base;
+        tie_run = tie_base;
+        uint32_t* oi = ws.ent_idx + row * ws.cap;
+        float* ov = ws.ent_val + row * ws.cap;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int64_t jb = j0 + (int64_t)(t * 64 + lane) * 4;
+            bool gt[4], eq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t k = mag_key(v[t][q]);
+                const bool inb = (jb + q) < d;
+                gt[q] = inb && (EXACT ? k > T : k >= T);
+                eq[q] = inb && EXACT && k == T;
+            }
+            if (EXACT) {
+                uint64_t m[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m[q] = __ballot(eq[q]);
+                const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                uint32_t before = __popcll(m[0] & lt) + __popcll(m[1] & lt) + __popcll(m[2] & lt) + __popcll(m[3] & lt);
+                uint32_t inlane = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (eq[q]) gt[q] = (tie_run + before + inlane) < tie_need;
+                    inlane += eq[q] ? 1u : 0u;
+                }
+                tie_run += __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t m = __ballot(gt[q]);
+                if (gt[q]) {
+                    const uint32_t pos = run + (uint32_t)__popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+                    oi[pos] = (uint32_t)(jb + q);
+                    ov[pos] = v[t][q];
+                }
+                run += (uint32_t)__popcll(m);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Radix passes over candidate lists (fast path) or full rows (exact path)
+// ------------------------------------------------------------------------------------------
+// Histogram of pass p over row data; grid-stride over (row, block of 64 K elements).
+template <bool FULLROW>
+__global__ __launch_bounds__(256) void k_radix_hist(RowSrc rows, int64_t n, int64_t d, int p, SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    constexpr int64_t BLK = 65536;
+    const int64_t nrows = FULLROW ? (int64_t)(*ws.nwork) : n;
+    const int64_t maxlen = FULLROW ? d : ws.cap;
+    const int64_t bpr = (maxlen + BLK - 1) / BLK;
+    const int64_t items = nrows * bpr;
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int64_t li = it / bpr;
+        const int64_t row = FULLROW ? (int64_t)ws.worklist[li] : li;
+        if (!FULLROW && ws.flags[row]) continue;
+        const int64_t len = FULLROW ? d : (int64_t)ws.rowcnt[row];
+        const int64_t b0 = (it % bpr) * BLK;
+        if (b0 >= len) continue;
+        const int64_t b1 = min(len, b0 + BLK);
+        for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
+        __syncthreads();
+        const uint32_t prefix = ws.prefix[row];
+        const float* src = FULLROW ? rows.row(row) : (ws.ent_val + row * ws.cap);
+        for (int64_t j = b0 + threadIdx.x; j < b1; j += 256) {
+            const uint32_t k = mag_key(src[j]);
+            if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
+        }
+        __syncthreads();
+        uint32_t* gh = ws.hist + row * HBINS;
+        for (int i = threadIdx.x; i < HBINS; i += 256)
+            if (h[i]) atomicAdd(&gh[i], h[i]);
+        __syncthreads();
+    }
+}
+
+// Select step of pass p: one workgroup per row.  After pass 2: thr = exact K-th key,
+// krem = ties to admit.  Fast path: a short list (count < K) or ambiguous ties -> worklist.
+template <bool FULLROW>
+__global__ __launch_bounds__(256) void k_radix_select(int64_t n, int p, int64_t K, SelWs ws) {
+    __shared__ uint32_t scratch[260];
+    const int64_t nrows = FULLROW ? (int64_t)(*ws.nwork) : n;
+    for (int64_t li = blockIdx.x; li < nrows; li += gridDim.x) {
+        const int64_t row = FULLROW ? (int64_t)ws.worklist[li] : li;
+        if (!FULLROW && ws.flags[row]) continue;
+        uint32_t* gh = ws.hist + row * HBINS;
+        if (!FULLROW && p == 0 && ws.rowcnt[row] < (uint32_t)K) {   // sample threshold too high
+            for (int i = threadIdx.x; i < HBINS; i += 256) gh[i] = 0;
+            if (threadIdx.x == 0) ws.flags[row] |= F_SHORT;
+            continue;
+        }
+        const uint32_t k = (p == 0) ? (uint32_t)K : ws.krem[row];
+        uint32_t bin, above;
+        hist_find(gh, k, bin, above, scratch);
+        const uint32_t ties_here = gh[bin];
+        __syncthreads();
+        for (int i = threadIdx.x; i < HBINS; i += 256) gh[i] = 0;    // ready for the next pass
+        if (threadIdx.x == 0) {
+            const uint32_t pre = (p == 0) ? 0u : ws.prefix[row];
+            ws.prefix[row] = (pre << pass_bits(p)) | bin;
+            ws.krem[row] = k - above;
+            if (p == 2) {
+                ws.thr[row] = ws.prefix[row];
+                if (ties_here > k - above) ws.flags[row] |= (FULLROW ? F_TIES | F_EXACT : F_TIES);
+                else if (FULLROW) ws.flags[row] |= F_EXACT;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// RowSrc that failed the fast path go on the worklist; their list state is reset.
+__global__ void k_build_worklist(int64_t n, int64_t K, int64_t d, SelWs ws, int force_all) {
+    // single block
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (int64_t row = threadIdx.x; row < n; row += blockDim.x) {
+        uint32_t f = ws.flags[row];
+        if (force_all || f) {
+            uint32_t pos = atomicAdd(&cnt, 1u);
+            ws.worklist[pos] = (uint32_t)row;
+            ws.flags[row] = F_EXACT;
+            ws.rowcnt[row] = 0;
+            ws.prefix[row] = 0;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *ws.nwork = cnt;
+}
+
+// Exact path, ambiguous ties: per chunk count of key == thr, then the exclusive prefix over
+// chunks (in index order) per row.  RowSrc without F_TIES get tieprefix = 0 (krem admits all ties).
+__global__ __launch_bounds__(256) void k_tie_count(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
+    const int64_t C = nchunks(d);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nrows = *ws.nwork;
+    const int64_t bpr = (C + 3) / 4;
+    for (int64_t it = blockIdx.x; it < nrows * bpr; it += gridDim.x) {
+        const int64_t row = ws.worklist[it / bpr];
+        const int64_t c = (it % bpr) * 4 + wv;
+        if (c >= C) continue;
+        uint32_t cnt = 0;
+        if (ws.flags[row] & F_TIES) {
+            const uint32_t T = ws.thr[row];
+            const float* r = rows.row(row);
+            const int64_t j1 = min(d, (c + 1) * (int64_t)CHUNK);
+            for (int64_t j = c * CHUNK + lane; j < j1; j += 64) cnt += (mag_key(r[j]) == T) ? 1u : 0u;
+            cnt = wave_sum(cnt);
+        }
+        if (lane == 0) ws.tieprefix[c * n + row] = cnt;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_tie_scan(int64_t n, int64_t d, SelWs ws) {
+    const int64_t C = nchunks(d);
+    const int64_t nrows = *ws.nwork;
+    for (int64_t li = blockIdx.x; li < nrows; li += gridDim.x) {
+        const int64_t row = ws.worklist[li];
+        if (threadIdx.x != 0) continue;
+        uint32_t run = 0;
+        for (int64_t c = 0; c < C; ++c) {
+            uint32_t v = ws.tieprefix[c * n + row];
+            ws.tieprefix[c * n + row] = run;
+            run += v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// RandK lists
+// ------------------------------------------------------------------------------------------
+__device__ inline int64_t randk_index(const flc_pattern& pat, const Feistel& fe, int64_t row, int64_t t,
+                                      int64_t ldi) {
+    return pat.d_randk_idx ? pat.d_randk_idx[row * ldi + t] : (int64_t)fe((uint64_t)t);
+}
+
+__global__ __launch_bounds__(256) void k_randk_count(int64_t n, int64_t d, int64_t K, flc_pattern pat,
+                                                     int64_t ldi, uint64_t seed, SelWs ws) {
+    const int64_t row = blockIdx.y;
+    Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
+        int64_t j = randk_index(pat, fe, row, t, ldi);
+        atomicAdd(&ws.cursor[(j >> CHUNK_SHIFT) * n + row], 1u);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_randk_scan(int64_t n, int64_t d, SelWs ws) {
+    const int64_t C = nchunks(d);
+    const int64_t row = blockIdx.x;
+    if (threadIdx.x != 0 || row >= n) return;
+    uint32_t run = 0;
+    for (int64_t c = 0; c < C; ++c) {
+        uint32_t v = ws.cursor[c * n + row];
+        ws.tab[c * n + row] = make_uint2(run, v);
+        ws.cursor[c * n + row] = 0;
+        run += v;
+    }
+    ws.thr[row] = 0;
+    ws.rowcnt[row] = run;
+}
+
+__global__ __launch_bounds__(256) void k_randk_scatter(RowSrc rows, int64_t n, int64_t d, int64_t K, flc_pattern pat,
+                                                       int64_t ldi, uint64_t seed, float scale, SelWs ws) {
+    const int64_t row = blockIdx.y;
+    Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
+    const float* r = rows.row(row);
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
+        const int64_t j = randk_index(pat, fe, row, t, ldi);
+        const int64_t slot = (j >> CHUNK_SHIFT) * n + row;
+        const uint32_t pos = ws.tab[slot].x + atomicAdd(&ws.cursor[slot], 1u);
+        ws.ent_idx[row * ws.cap + pos] = (uint32_t)j;
+        ws.ent_val[row * ws.cap + pos] = scale * r[j];      // (D/K) * x[S] in fp32
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Chunk-owner accumulation.  One wave per chunk, fp32 tile in LDS; rows folded in order.
+// ASSIGN (single row, no weights): out = tile with the entry values stored, not added
+// (keeps -0.0 like torch's out[ind] = x[ind]).
+// ------------------------------------------------------------------------------------------
+template <bool ASSIGN>
+__global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
+                                                     float wt, float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float tile[4][CHUNK];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t C = nchunks(d);
+    float* tl = tile[wv];
+    constexpr int PF = 16;                 // rows whose first 64 entries are in flight together
+    for (int64_t c = (int64_t)blockIdx.x * 4 + wv; c < C; c += (int64_t)gridDim.x * 4) {
+        // waves are independent: each owns its tile, LDS ops of one wave retire in order
+        for (int i = lane; i < CHUNK; i += 64) tl[i] = 0.f;
+        {
+            const int64_t cbase = c * CHUNK;
+            for (int64_t i0 = 0; i0 < n; i0 += PF) {
+                // lanes 0..PF-1 fetch the table entries of rows i0..i0+PF-1
+                uint2 te = make_uint2(0, 0);
+                uint32_t tthr = 0;
+                float tw = 1.f;
+                if (lane < PF && i0 + lane < n) {
+                    te = ws.tab[c * n + i0 + lane];
+                    tthr = ws.thr[i0 + lane];
+                    tw = w ? w[i0 + lane] : 1.f;
+                }
+                uint32_t e_idx[PF];
+                float e_val[PF];
+#pragma unroll
+                for (int q = 0; q < PF; ++q) {
+                    const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
+                    e_idx[q] = 0;
+                    e_val[q] = 0.f;
+                    if ((uint32_t)lane < cnt && i0 + q < n) {
+                        e_idx[q] = ws.ent_idx[(i0 + q) * ws.cap + off + lane];
+                        e_val[q] = ws.ent_val[(i0 + q) * ws.cap + off + lane];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < PF; ++q) {
+                    if (i0 + q >= n) break;
+                    const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
+                    const uint32_t T = __shfl(tthr, q, WAVE);
+                    const float wi = __shfl(tw, q, WAVE);
+                    if ((uint32_t)lane < cnt && mag_key(e_val[q]) >= T) {
+                        const int loc = (int)(e_idx[q] - (uint32_t)cbase);
+                        if (ASSIGN) tl[loc] = e_val[q];
+                        else tl[loc] = tl[loc] + wi * e_val[q];
+                    }
+                    for (uint32_t e = 64 + lane; e < cnt; e += 64) {     // long lists (rare)
+                        const uint32_t ix = ws.ent_idx[(i0 + q) * ws.cap + off + e];
+                        const float vv = ws.ent_val[(i0 + q) * ws.cap + off + e];
+                        if (mag_key(vv) >= T) {
+                            const int loc = (int)(ix - (uint32_t)cbase);
+                            if (ASSIGN) tl[loc] = vv;
+                            else tl[loc] = tl[loc] + wi * vv;
+                        }
+                    }
+                }
+            }
+            const int64_t len = min((int64_t)CHUNK, d - cbase);
+            for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host orchestration
+// ------------------------------------------------------------------------------------------
+static int64_t host_chunks(int64_t d) { return (d + CHUNK - 1) / CHUNK; }
+
+int64_t sel_capacity(int codec, int64_t d, int64_t K) {
+    if (codec == FLC_RANDK) return std::max<int64_t>(K, 1);
+    // candidates of the fast path (~K (1 + 4/sqrt(ks))) with margin; the exact path needs K + CHUNK
+    int64_t cap = 2 * K + 2 * CHUNK;
+    return std::min<int64_t>(std::max<int64_t>(cap, 1), std::max<int64_t>(d, 1));
+}
+
+static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, size_t* bytes) {
+    Carver cv(base);
+    const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
+    SelWs s;
+    s.cap = sel_capacity(codec, d, K);
+    s.tab = cv.take<uint2>((size_t)C * nn);
+    s.ent_idx = cv.take<uint32_t>((size_t)nn * s.cap);
+    s.ent_val = cv.take<float>((size_t)nn * s.cap);
+    s.rowcnt = cv.take<uint32_t>(nn);
+    s.flags = cv.take<uint32_t>(nn);
+    s.thr = cv.take<uint32_t>(nn);
+    s.prefix = cv.take<uint32_t>(nn);
+    s.krem = cv.take<uint32_t>(nn);
+    s.worklist = cv.take<uint32_t>(nn);
+    s.nwork = cv.take<uint32_t>(4);
+    if (codec == FLC_TOPK) {
+        s.tieprefix = cv.take<uint32_t>((size_t)C * nn);
+        s.hist = cv.take<uint32_t>((size_t)nn * HBINS);
+        s.cursor = nullptr;
+    } else {
+        s.tieprefix = nullptr;
+        s.hist = nullptr;
+        s.cursor = cv.take<uint32_t>((size_t)C * nn);
+    }
+    if (bytes) *bytes = cv.bytes();
+    return s;
+}
+
+size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
+    size_t b = 0;
+    carve_sel(nullptr, prm->codec, n, d, prm->k, &b);
+    return b;
+}
+
+static int grid_stride_blocks(int64_t items, int64_t cap = 4096) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(items, cap));
+}
+
+// Runs the TopK / RandK pipeline for n rows and writes out (ASSIGN: n == 1 dense encode).
+int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
+            bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
+    const int codec = prm->codec;
+    const int64_t K = prm->k;
+    if (d == 0) return FLC_OK;
+    if (n == 0) { FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st)); return FLC_OK; }
+    if (K < 1 || K > d) { set_error("K=%lld outside [1, D=%lld]", (long long)K, (long long)d); return FLC_ERR_ARG; }
+    if (d >= (int64_t)0xFFFFFFFF) { set_error("D too large for 32-bit entry indices"); return FLC_ERR_ARG; }
+    size_t need = 0;
+    carve_sel(nullptr, codec, n, d, K, &need);
+    if (ws_bytes < need) { set_error("select: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
+    SelWs ws = carve_sel(wsp, codec, n, d, K, nullptr);
+    const int64_t C = host_chunks(d);
+    if (codec == FLC_RANDK) {
+        const int64_t ldi = (pat && pat->idx_ld) ? pat->idx_ld : K;
+        flc_pattern p = pat ? *pat : flc_pattern{};
+        FLC_CHECK_HIP(hipMemsetAsync(ws.cursor, 0, (size_t)C * n * sizeof(uint32_t), st));
+        dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>((K + 255) / 256, 64)), (unsigned)n);
+        hipLaunchKernelGGL(k_randk_count, g, dim3(256), 0, st, n, d, K, p, ldi, prm->seed, ws);
+        FLC_CHECK_LAUNCH("k_randk_count");
+        hipLaunchKernelGGL(k_randk_scan, dim3((unsigned)n), dim3(64), 0, st, n, d, ws);
+        FLC_CHECK_LAUNCH("k_randk_scan");
+        { ProfScope _ps("k_randk_scatter", st);
+hipLaunchKernelGGL(k_randk_scatter, g, dim3(256), 0, st, rows, n, d, K, p, ldi, prm->seed, prm->randk_scale, ws); }
+        FLC_CHECK_LAUNCH("k_randk_scatter");
+    } else {  // TOPK
+        FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
+        const bool dense_k = K * 16 > d;   // large K: the candidate list would not be smaller than the row
+        const int64_t bpr = (C + 3) / 4;
+        if (!dense_k) {
+            { ProfScope _ps("k_topk_sample", st);
+hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, K, ws); }
+            FLC_CHECK_LAUNCH("k_topk_sample");
+            int gb = grid_stride_blocks(n * bpr, 8192);
+            { ProfScope _ps("k_topk_filter", st);
+if (vec) hipLaunchKernelGGL((k_topk_filter<false, true>), dim3(gb), dim3(256), 0, st, rows, n, d, ws);
+            else hipLaunchKernelGGL((k_topk_filter<false, false>), dim3(gb), dim3(256), 0, st, rows, n, d, ws); }
+            FLC_CHECK_LAUNCH("k_topk_filter");
+            const int64_t hb = (ws.cap + 65535) / 65536;
+            for (int p = 0; p < 3; ++p) {
+                { ProfScope _ps("k_radix_hist", st);
+hipLaunchKernelGGL((k_radix_hist<false>), dim3(grid_stride_blocks(n * hb)), dim3(256), 0, st, rows, n, d, p, ws); }
+                FLC_CHECK_LAUNCH("k_radix_hist");
+                hipLaunchKernelGGL((k_radix_select<false>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, p, K, ws);
+                FLC_CHECK_LAUNCH("k_radix_select");
+            }
+        } else {
+            FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
+        }
+        // exact path for failed rows (all rows when dense_k)
+        hipLaunchKernelGGL(k_build_worklist, dim3(1), dim3(1024), 0, st, n, K, d, ws, dense_k ? 1 : 0);
+        FLC_CHECK_LAUNCH("k_build_worklist");
+        const int64_t hb = (d + 65535) / 65536;
+        for (int p = 0; p < 3; ++p) {
+            { ProfScope _ps("k_radix_hist_full", st);
+hipLaunchKernelGGL((k_radix_hist<true>), dim3(grid_stride_blocks(n * hb)), dim3(256), 0, st, rows, n, d, p, ws); }
+            FLC_CHECK_LAUNCH("k_radix_hist(full)");
+            hipLaunchKernelGGL((k_radix_select<true>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, p, K, ws);
+            FLC_CHECK_LAUNCH("k_radix_select(full)");
+        }
+        hipLaunchKernelGGL(k_tie_count, dim3(grid_stride_blocks(n * bpr, 4096)), dim3(256), 0, st, rows, n, d, ws);
+        FLC_CHECK_LAUNCH("k_tie_count");
+        hipLaunchKernelGGL(k_tie_scan, dim3(grid_stride_blocks(n, 1024)), dim3(64), 0, st, n, d, ws);
+        FLC_CHECK_LAUNCH("k_tie_scan");
+        int gb = grid_stride_blocks(n * bpr, 8192);
+        { ProfScope _ps("k_topk_filter_exact", st);
+if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0, st, rows, n, d, ws);
+        else hipLaunchKernelGGL((k_topk_filter<true, false>), dim3(gb), dim3(256), 0, st, rows, n, d, ws); }
+        FLC_CHECK_LAUNCH("k_topk_filter(exact)");
+    }
+    // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
+    // below the exact threshold; k_chunk_accum admits key >= thr.
+    const int ab = grid_stride_blocks((C + 3) / 4, 2048);
+    { ProfScope _ps("k_chunk_accum", st);
+if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out); }
+    FLC_CHECK_LAUNCH("k_chunk_accum");
+    return FLC_OK;
+}
+
+// Dense single-vector RandK: out = 0; out[S] = scale * x[S]  (compressors.py:242-243)
+__global__ __launch_bounds__(256) void k_randk_dense(const float* __restrict__ x, int64_t d, int64_t K, flc_pattern pat,
+                                                     uint64_t seed, float scale, float* __restrict__ out) {
+    Feistel fe(client_key(seed, pat.client0), (uint64_t)d);
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
+        const int64_t j = randk_index(pat, fe, 0, t, K);
+        out[j] = scale * x[j];
+    }
+}
+
+int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out,
+                hipStream_t st) {
+    if (d == 0) return FLC_OK;
+    if (prm->k < 1 || prm->k > d) { set_error("randk: K outside [1, D]"); return FLC_ERR_ARG; }
+    FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
+    flc_pattern p = pat ? *pat : flc_pattern{};
+    int g = (int)std::max<int64_t>(1, std::min<int64_t>((prm->k + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_randk_dense, dim3(g), dim3(256), 0, st, x, d, prm->k, p, prm->seed, prm->randk_scale, out);
+    FLC_CHECK_LAUNCH("k_randk_dense");
+    return FLC_OK;
+}
+
+}  // namespace flc

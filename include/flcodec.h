@@ -1,0 +1,167 @@
+/*
+ * flcodec — MI355X (gfx950) gradient codecs + N-way reduction: the C ABI.
+ *
+ * The drop-in boundary for FL_PyTorch's simulated-uplink hot path.  The reference is pure
+ * Python; the Python layer in flpytorch_amd/aggregation binds these entry points with ctypes
+ * (INTEGRATION.md shows the binding) and keeps the reference's object protocol on top:
+ *   - Compressor.generateCompressPattern / compressVector   fl_pytorch/utils/compressors.py:196-371
+ *   - <Algorithm>.serverGradient                           fl_pytorch/utils/algorithms.py:1748-1770,
+ *                                                          1810-1832 (+ the identical cores listed
+ *                                                          in SURVEY.md §8a row a14)
+ *
+ * Conventions
+ *   - every pointer named d_* is DEVICE memory (caller-owned; the library never frees it);
+ *     h_* is host memory.  fp32 data only (other dtypes: FLC_ERR_DTYPE).
+ *   - every compute call is asynchronous on `stream` (a hipStream_t, passed as void*), never
+ *     synchronises the device, never allocates: scratch comes from a caller workspace sized by
+ *     the matching *_workspace_size query.  Calls are reentrant across host threads that use
+ *     distinct streams and distinct workspaces.
+ *   - return 0 (FLC_OK) or an flc_status; flc_last_error_string() gives the detail for the
+ *     calling thread.
+ */
+#ifndef FLCODEC_H
+#define FLCODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    FLC_OK = 0,
+    FLC_ERR_ARG = 1,        /* bad size / null pointer / misaligned where alignment is required */
+    FLC_ERR_DTYPE = 2,      /* not fp32 */
+    FLC_ERR_HIP = 3,        /* a HIP runtime call failed (launch, memset) */
+    FLC_ERR_WORKSPACE = 4,  /* workspace smaller than *_workspace_size() */
+    FLC_ERR_UNSUPPORTED = 5 /* codec / mode not built (e.g. rank_k) */
+} flc_status;
+
+/* Codec ids = the reference's CompressorType values (compressors.py:11-19). */
+typedef enum {
+    FLC_IDENT = 1,
+    FLC_LAZY = 2,
+    FLC_RANDK = 3,
+    FLC_NATURAL = 4,
+    FLC_STD_DITHERING = 5,
+    FLC_NAT_DITHERING = 6,
+    FLC_TOPK = 7
+} flc_codec;
+
+/* p-norm used by the dithering codecs (Compressor.p, compressors.py:91, 123). */
+#define FLC_NORM_L1 1
+#define FLC_NORM_L2 2
+#define FLC_NORM_LINF 0
+
+/* Codec configuration — the constants Compressor.make* sets (compressors.py:64-178). */
+typedef struct {
+    int32_t codec;          /* flc_codec */
+    int32_t s;              /* dithering: number of level intervals (levels has s+1 entries) */
+    int32_t norm;           /* dithering: FLC_NORM_* */
+    int32_t reserved;
+    int64_t k;              /* randk / topk: K */
+    float lazy_p;           /* lazy: P */
+    float randk_scale;      /* randk: (float)(D / K) as the reference's fp32 scalar multiply */
+    const float* d_levels;  /* dithering: s+1 fp32 levels (Compressor.levelsValues) on device */
+    uint64_t seed;          /* device-RNG mode: experiment key of the counter-based generator */
+} flc_codec_params;
+
+/* Patterns: where the randomness of one call comes from (generateCompressPattern, 196-216).
+ * Compat mode reproduces the reference's numpy stream bit for bit (host-drawn, uploaded);
+ * device mode draws from a counter-based generator keyed by (seed, client id, element). */
+typedef struct {
+    const int64_t* d_randk_idx; /* randk compat: [n][k] int64 indices (numpy choice(D,K)) or NULL */
+    const double* d_uniforms;   /* natural / dithering compat: [n][d] float64 (numpy rand(D)) or NULL */
+    const double* d_lazy_u;     /* lazy: [n] float64 draws (numpy random()) on device — required */
+    int64_t client0;            /* device mode: id of row 0 (row r is client client0 + r) */
+    int64_t uniforms_ld;        /* leading dimension of d_uniforms (elements); 0 = d */
+    int64_t idx_ld;             /* leading dimension of d_randk_idx (elements); 0 = k */
+} flc_pattern;
+
+/* ----------------------------------------------------------------------------------------
+ * Library info / errors
+ * -------------------------------------------------------------------------------------- */
+int flc_version(void);                    /* ABI version (major*100 + minor) */
+const char* flc_last_error_string(void);  /* thread-local detail of the last failure */
+
+/* ----------------------------------------------------------------------------------------
+ * N-way reduction — the serverGradient core (algorithms.py:1753-1768).
+ *
+ *   mode FLC_REDUCE_REL_X : out = (sum_i w_i * (x - row_i)) / w_total      (client models in)
+ *   mode FLC_REDUCE_PLAIN : out = (sum_i w_i * row_i) / w_total            (client updates in)
+ *
+ * Summed per element strictly in row order with fp32 rounding after every operation, i.e.
+ * bit-identical to the reference's sequential loop (gs = w0*g0; gs += wi*gi; gs / w_total).
+ * d_w: n fp32 weights (the reference's python-float weights as fp32), or NULL for all 1.0.
+ * w_total: the python-float sum of the weights, as the fp32 divisor.
+ * Rows come either as a device array of n row pointers (flc_reduce_rows; every row pointer,
+ * d_x and d_out 16-byte aligned) or as one strided matrix (flc_reduce_matrix, row i at
+ * d_rows + i*ld; any alignment, the vector path needs 16-byte rows and ld % 4 == 0).
+ * -------------------------------------------------------------------------------------- */
+#define FLC_REDUCE_PLAIN 0
+#define FLC_REDUCE_REL_X 1
+int flc_reduce_rows(const float* const* d_row_ptrs, int64_t n, int64_t d, const float* d_x,
+                    const float* d_w, float w_total, int mode, float* d_out, void* stream);
+int flc_reduce_matrix(const float* d_rows, int64_t ld, int64_t n, int64_t d, const float* d_x,
+                      const float* d_w, float w_total, int mode, float* d_out, void* stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Single-vector encode — Compressor.compressVector(x) (compressors.py:218-371): dense fp32
+ * output `d_out[d]` (zeros where the codec sends nothing).  `row` selects pattern row 0.
+ *   d_pnorm_in : dithering only — device fp32 norm to use instead of computing one (the norm
+ *                the server receives on the wire), or NULL
+ *   d_pnorm_out: dithering only — device fp32 where the norm used is written, or NULL
+ * -------------------------------------------------------------------------------------- */
+size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t d);
+int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+               const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws,
+               size_t ws_bytes, void* stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Fused batch encode + reduce — the simulated uplink of one round in one call:
+ *     out = (sum_i w_i * C_i(row_i)) / w_total
+ * with C_i the codec applied to client row i under its own pattern, summed in row order
+ * (bit-identical to reducing the dense compressVector outputs sequentially).  Rows are the
+ * strided matrix d_rows (row i at d_rows + i*ld, ld % 4 == 0 and 16-byte alignment for the
+ * vector path) — or, with d_rows == NULL, the device pointer array d_row_ptrs (every row
+ * 16-byte aligned).
+ * d_pnorms_out: optional [n] fp32 norms used (dithering).
+ * -------------------------------------------------------------------------------------- */
+size_t flc_encode_reduce_workspace_size(const flc_codec_params* prm, int64_t n, int64_t d);
+int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern* pat, const float* d_rows,
+                      int64_t ld, const float* const* d_row_ptrs, int64_t n, int64_t d,
+                      const float* d_w, float w_total, float* d_pnorms_out, float* d_out,
+                      void* d_ws, size_t ws_bytes, void* stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Host side of compat mode: the numpy legacy MT19937 stream (what the reference's
+ * rndgen.choice / rand / random / randint draw, compressors.py:204-212, algorithms.py:2055),
+ * advanced in place on a caller-held state (key[624], pos — numpy's get_state() layout).
+ * Each call consumes exactly the draws numpy would, so the caller can hand the state back
+ * to its RandomState (set_state) and the experiment stream stays identical.
+ * h_scratch for choice: n int64 (the Fisher-Yates array).
+ * -------------------------------------------------------------------------------------- */
+int flc_mt_choice(uint32_t* h_key, int32_t* h_pos, int64_t n, int64_t k, int64_t* h_out,
+                  int64_t* h_scratch);
+int flc_mt_rand(uint32_t* h_key, int32_t* h_pos, int64_t n, double* h_out);
+int flc_mt_randint31(uint32_t* h_key, int32_t* h_pos, int64_t count, int64_t* h_out);
+
+/* Device-RNG mode, host mirror: the uniform / index the kernels draw for (seed, client, j). */
+double flc_device_uniform(uint64_t seed, int64_t client, int64_t j);
+int flc_device_randk_indices(uint64_t seed, int64_t client, int64_t d, int64_t k, int64_t* h_out);
+
+/* ----------------------------------------------------------------------------------------
+ * Kernel timing (off by default).  While enabled, every launch of the named hot kernels is
+ * bracketed by hipEvents recorded on the launch stream; flc_profile_collect() waits for them
+ * and returns the summed duration and launch count for one kernel name, then forgets them.
+ * Names: k_topk_filter, k_topk_sample, k_radix_hist, k_chunk_accum, k_ew_accum_vec,
+ * k_norm_partials, k_reduce_vec, k_randk_scatter.
+ * -------------------------------------------------------------------------------------- */
+int flc_profile_enable(int on);
+int flc_profile_collect(const char* kernel, double* h_total_ms, int64_t* h_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLCODEC_H */

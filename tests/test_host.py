@@ -1,0 +1,119 @@
+"""CPU tests of the product's host side: the C ABI exports, the compat-mode numpy stream and the
+Compressor protocol constants (no GPU compute is called here)."""
+import math
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from flpytorch_amd import _lib
+from flpytorch_amd import aggregation as ag
+from oracle import codecs as oc
+from oracle.rng import OracleRandomState
+from tests.golden_io import load
+
+HEADER = __import__("os").path.join(__import__("os").path.dirname(__file__), "..", "include", "flcodec.h")
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    declared = set(re.findall(r"\b(flc_[a-z0-9_]+)\s*\(", open(HEADER).read()))
+    assert declared == set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.flc_version() == 100
+
+
+def test_library_is_gfx950():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+@pytest.mark.parametrize("seed", [0, 1, 123, 2 ** 32 - 1])
+def test_stream_matches_numpy_and_oracle(seed):
+    rs_np = np.random.RandomState(seed)
+    rs_ag = np.random.RandomState(seed)
+    rs_or = OracleRandomState(seed)
+    for (n, k) in [(1, 1), (10, 10), (1000, 10), (2465, 247), (70000, 700)]:
+        a = ag.stream_choice(rs_ag, n, k)
+        np.testing.assert_array_equal(a, rs_np.choice(n, k, replace=False))
+        np.testing.assert_array_equal(a, rs_or.choice(n, k))
+        assert int(ag.stream_randint31(rs_ag)[0]) == rs_np.randint(2 ** 31) == rs_or.randint31()
+    np.testing.assert_array_equal(ag.stream_rand(rs_ag, 1001), rs_np.rand(1001))
+    assert ag.stream_random(rs_ag) == rs_np.random()
+    # the RandomState object itself continues the same stream afterwards
+    np.testing.assert_array_equal(rs_ag.randint(0, 1000, 50), rs_np.randint(0, 1000, 50))
+
+
+def test_stream_rejects_other_generators():
+    with pytest.raises((TypeError, AttributeError)):
+        ag.stream_choice(np.random.default_rng(0), 10, 3)
+
+
+CODEC_META, _ = load("codecs")
+
+
+@pytest.mark.parametrize("m", CODEC_META, ids=[f"{m['spec']}-{m['D']}" for m in CODEC_META])
+def test_compressor_constants_match_reference(m):
+    c = ag.initCompressor(m["spec"], m["D"])
+    assert c.compressorType == m["type"]
+    assert c.fullName() == m["fullName"]
+    assert getattr(c, "K", None) == m["K"]
+    assert getattr(c, "w", None) == m["w"]
+    assert getattr(c, "alpha", None) == m["alpha"]
+    assert c.isUnbiasedCompressor() == m["isUnbiased"]
+    assert c.isContractionCompressor() == m["isContraction"]
+    if m["type"] in (5, 6):
+        assert c.s == m["s"] and float(c.p) == m["p"]
+        np.testing.assert_array_equal(c.levelsValues.numpy(), oc.OracleCompressor(m["spec"], m["D"]).levels)
+
+
+def test_unknown_spec_raises_assertion():
+    with pytest.raises(AssertionError):
+        ag.initCompressor("gzip:9", 10)
+
+
+def test_rank_k_constants():
+    c = ag.initCompressor("rank_k:100%", 8)
+    assert (c.A, c.B, c.K) == (2, 4, 8) and c.alpha == 4.0   # A = first divisor >= int(sqrt(D))
+
+
+def test_generate_pattern_advances_stream_like_reference():
+    rs_a, rs_b = np.random.RandomState(5), np.random.RandomState(5)
+    for spec, draw in [("randk:10%", lambda r: r.choice(100, 10, replace=False)),
+                       ("qsgd:4", lambda r: r.rand(100)), ("bernulli:0.3", lambda r: r.random()),
+                       ("natural", lambda r: r.rand(100)), ("topk:5", lambda r: None), ("ident", lambda r: None)]:
+        c = ag.initCompressor(spec, 100)
+        c.generateCompressPattern(rs_a, "cpu", 0, None)
+        ref = draw(rs_b)
+        if spec.startswith("randk"):
+            np.testing.assert_array_equal(c.S.numpy(), ref)
+        elif spec.startswith(("qsgd", "natural")):
+            np.testing.assert_array_equal(c.testp.numpy(), ref)
+        elif spec.startswith("bernulli"):
+            assert c.testp == ref
+    assert rs_a.randint(2 ** 31) == rs_b.randint(2 ** 31)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_compute_without_gpu_fails_loudly():
+    c = ag.initCompressor("topk:1", 10)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        c.compressVector(torch.ones(10))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ag.reduce_rows(torch.ones(4), [torch.ones(4)])
+    # identity stays an alias, like the reference (compressors.py:228): no compute involved
+    x = torch.ones(3)
+    assert ag.initCompressor("ident", 3).compressVector(x) is x
+
+
+def test_device_rng_host_mirror():
+    lib = _lib.load()
+    for d, k in [(1, 1), (7, 3), (1000, 10), (4097, 4097), (1 << 20, 10486)]:
+        idx = np.empty(k, dtype=np.int64)
+        assert lib.flc_device_randk_indices(42, 3, d, k, idx.ctypes.data) == 0
+        assert idx.min() >= 0 and idx.max() < d and np.unique(idx).size == k
+    u = np.array([lib.flc_device_uniform(42, 3, j) for j in range(20000)])
+    assert u.min() >= 0.0 and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01
+    assert math.isclose(np.var(u), 1 / 12, rel_tol=0.03)
