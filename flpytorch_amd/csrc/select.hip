@@ -60,6 +60,7 @@ __device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, u
     uint32_t s = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) { local[q] = h[HBINS - 1 - (t * 8 + q)]; s += local[q]; }
+    if (t == 0) { scratch[256] = 0; scratch[257] = 0; }   // defined result even if k > total
     scratch[t] = s;
     __syncthreads();
     // inclusive scan (Hillis-Steele) over 256 thread sums
