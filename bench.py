@@ -129,15 +129,17 @@ def main():
     red = ag.UplinkReducer(comp, device=dev, seed=20241015)
     client0 = rank * n
 
+    if world > 1:
+        from flpytorch_amd.sharding import ShardedUplink, product_partial
+        # local partial = sum_i C_i(row_i) in client order (fp32 divisor 1.0 keeps it exact),
+        # one RCCL all-reduce of D floats over xGMI, then the global mean
+        uplink = ShardedUplink(product_partial(red), mode="allreduce")
+
     def step():
         if world == 1:
             red(rows, out=out, client0=client0)
         else:
-            # local partial = sum_i C_i(row_i) in client order (fp32 divisor 1.0 keeps it exact),
-            # one RCCL sum over the ranks, then the global mean
-            red(rows, out=out, client0=client0, divisor=1.0)
-            dist.all_reduce(out)
-            out.div_(float(n * world))
+            uplink(rows, client0=client0, total_weight=float(n * world), out=out)
 
     for _ in range(args.warmup):
         step()

@@ -25,6 +25,7 @@ EXPORTS = [
     "flc_mt_choice", "flc_mt_rand", "flc_mt_randint31",
     "flc_device_uniform", "flc_device_randk_indices",
     "flc_profile_enable", "flc_profile_collect",
+    "flc_selftest_division",
 ]
 
 
@@ -95,6 +96,7 @@ def load():
         lib.flc_device_randk_indices.argtypes = [ctypes.c_uint64, i64, i64, i64, vp]
         lib.flc_profile_enable.argtypes = [i32]
         lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
+        lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
         for name in EXPORTS:
             if name not in ("flc_version", "flc_last_error_string", "flc_device_uniform",
                             "flc_encode_workspace_size", "flc_encode_reduce_workspace_size"):

@@ -98,6 +98,16 @@ extern "C" int flc_profile_collect(const char* kernel, double* h_total_ms, int64
 
 extern "C" const char* flc_last_error_string(void) { return g_err; }
 
+namespace flc {
+int selftest_division(const float* d_b, int nb, unsigned long long* d_bad, hipStream_t st);
+}
+extern "C" int flc_selftest_division(const float* d_divisors, int n, unsigned long long* d_mismatches,
+                                     void* stream) {
+    if (n < 0 || (n > 0 && (!d_divisors || !d_mismatches))) { set_error("flc_selftest_division: bad args"); return FLC_ERR_ARG; }
+    if (n == 0) return FLC_OK;
+    return selftest_division(d_divisors, n, d_mismatches, (hipStream_t)stream);
+}
+
 extern "C" size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t d) {
     if (!prm || !known(prm->codec)) return 0;
     if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);

@@ -14,6 +14,9 @@
 //   (y * sign) * pnorm (the reference's line 326); natural uses a correctly rounded fp32 log2.
 // Norms accumulate in float64 (exactly rounded fp32 result); torch's CPU norm is not
 // (see DESIGN.md), so parity is stated against the exactly rounded norm.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.hpp"
 
 namespace flc {
@@ -36,65 +39,99 @@ __device__ inline double ncomb(double a, double b) {
     return a + b;
 }
 
+// nonzero |v| below 2^-80: the row cannot use the unguarded fast division (div_fast)
+__device__ inline uint32_t is_tiny(float v) { const float a = fabsf(v); return (a != 0.f && a < 0x1p-80f) ? 1u : 0u; }
+
 template <int NORM, bool VEC>
 __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, int64_t d, int64_t parts,
-                                                       double* __restrict__ partial) {
+                                                       double* __restrict__ partial, uint32_t* __restrict__ tinyp) {
     const int64_t row = blockIdx.y;
     const float* r = src.row(row);
     __shared__ double red[4];
+    __shared__ uint32_t redt[4];
     for (int64_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const int64_t j0 = part * NORM_PART;
         const int64_t j1 = min(d, j0 + (int64_t)NORM_PART);
         double a = 0.0;
+        uint32_t tiny = 0;
         if (VEC) {
             const int64_t g0 = j0 / 4, g1 = j1 / 4;   // j0 % 4 == 0 (NORM_PART % 4 == 0)
             for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
                 float4 v = reinterpret_cast<const float4*>(r)[g];
                 a = nacc<NORM>(a, v.x); a = nacc<NORM>(a, v.y); a = nacc<NORM>(a, v.z); a = nacc<NORM>(a, v.w);
+                tiny |= is_tiny(v.x) | is_tiny(v.y) | is_tiny(v.z) | is_tiny(v.w);
             }
-            for (int64_t j = g1 * 4 + threadIdx.x; j < j1; j += 256) a = nacc<NORM>(a, r[j]);
+            for (int64_t j = g1 * 4 + threadIdx.x; j < j1; j += 256) { a = nacc<NORM>(a, r[j]); tiny |= is_tiny(r[j]); }
         } else {
-            for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) a = nacc<NORM>(a, r[j]);
+            for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) { a = nacc<NORM>(a, r[j]); tiny |= is_tiny(r[j]); }
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) a = ncomb<NORM>(a, __shfl_xor(a, o, WAVE));
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+        for (int o = 32; o > 0; o >>= 1) {
+            a = ncomb<NORM>(a, __shfl_xor(a, o, WAVE));
+            tiny |= __shfl_xor(tiny, o, WAVE);
+        }
+        if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = a; redt[threadIdx.x >> 6] = tiny; }
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             partial[row * parts + part] = ncomb<NORM>(ncomb<NORM>(red[0], red[1]), ncomb<NORM>(red[2], red[3]));
+            tinyp[row * parts + part] = redt[0] | redt[1] | redt[2] | redt[3];
+        }
         __syncthreads();
     }
 }
 
+// Per row: the norm, RN(1/norm), rowfast = 1 when the encode may divide by the norm with the
+// unguarded div_fast (norm inside [2^-40, 2^80], no nonzero element below 2^-80), and the
+// device-RNG row key.
 template <int NORM>
-__global__ __launch_bounds__(64) void k_norm_final(const double* __restrict__ partial, int64_t parts,
-                                                   int64_t n, float* __restrict__ pn) {
+__global__ __launch_bounds__(64) void k_norm_final(const double* __restrict__ partial,
+                                                   const uint32_t* __restrict__ tinyp, int64_t parts,
+                                                   int64_t n, float* __restrict__ pn, float* __restrict__ rpn,
+                                                   uint32_t* __restrict__ rowfast, uint64_t seed, int64_t client0,
+                                                   uint32_t* __restrict__ rk) {
     const int64_t row = blockIdx.x;
     if (row >= n) return;
     double a = 0.0;
-    for (int64_t p = threadIdx.x; p < parts; p += 64) a = ncomb<NORM>(a, partial[row * parts + p]);
+    uint32_t tiny = 0;
+    for (int64_t p = threadIdx.x; p < parts; p += 64) {
+        a = ncomb<NORM>(a, partial[row * parts + p]);
+        tiny |= tinyp[row * parts + p];
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) a = ncomb<NORM>(a, __shfl_xor(a, o, WAVE));
-    if (threadIdx.x == 0) pn[row] = (NORM == FLC_NORM_L2) ? (float)sqrt(a) : (float)a;
+    for (int o = 32; o > 0; o >>= 1) {
+        a = ncomb<NORM>(a, __shfl_xor(a, o, WAVE));
+        tiny |= __shfl_xor(tiny, o, WAVE);
+    }
+    if (threadIdx.x == 0) {
+        const float v = (NORM == FLC_NORM_L2) ? (float)sqrt(a) : (float)a;
+        pn[row] = v;
+        rpn[row] = 1.0f / v;
+        rowfast[row] = (!tiny && v >= 0x1p-40f && v <= 0x1p80f) ? 1u : 0u;
+        rk[row] = rowkey(client_key(seed, client0 + row));
+    }
 }
 
 int64_t norm_parts(int64_t d) { return (d + NORM_PART - 1) / NORM_PART; }
 
-int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* partial, float* pn,
+int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* partial, uint32_t* tinyp,
+                 float* pn, float* rpn, uint32_t* rowfast, uint64_t seed, int64_t client0, uint32_t* rk,
                  hipStream_t st) {
     const int64_t parts = norm_parts(d);
     if (n == 0) return FLC_OK;
     if (parts == 0) {  // d == 0: norm of an empty vector
         FLC_CHECK_HIP(hipMemsetAsync(pn, 0, (size_t)n * sizeof(float), st));
+        FLC_CHECK_HIP(hipMemsetAsync(rowfast, 0, (size_t)n * sizeof(uint32_t), st));
+        FLC_CHECK_HIP(hipMemsetAsync(rk, 0, (size_t)n * sizeof(uint32_t), st));
         return FLC_OK;
     }
     dim3 grid((unsigned)std::min<int64_t>(parts, 64), (unsigned)n);
 #define FLC_NORM_CASE(NK)                                                                           \
     { ProfScope _ps("k_norm_partials", st);                                                         \
-    if (vec) hipLaunchKernelGGL((k_norm_partials<NK, true>), grid, dim3(256), 0, st, src, d, parts, partial); \
-    else hipLaunchKernelGGL((k_norm_partials<NK, false>), grid, dim3(256), 0, st, src, d, parts, partial); }  \
+    if (vec) hipLaunchKernelGGL((k_norm_partials<NK, true>), grid, dim3(256), 0, st, src, d, parts, partial, tinyp); \
+    else hipLaunchKernelGGL((k_norm_partials<NK, false>), grid, dim3(256), 0, st, src, d, parts, partial, tinyp); } \
     FLC_CHECK_LAUNCH("k_norm_partials");                                                            \
-    hipLaunchKernelGGL((k_norm_final<NK>), dim3((unsigned)n), dim3(64), 0, st, partial, parts, n, pn);  \
+    hipLaunchKernelGGL((k_norm_final<NK>), dim3((unsigned)n), dim3(64), 0, st, partial, tinyp, parts, n, pn, rpn,   \
+                       rowfast, seed, client0, rk);                                                 \
     FLC_CHECK_LAUNCH("k_norm_final");
     if (norm == FLC_NORM_L2) { FLC_NORM_CASE(FLC_NORM_L2) }
     else if (norm == FLC_NORM_L1) { FLC_NORM_CASE(FLC_NORM_L1) }
@@ -104,92 +141,244 @@ int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* p
 }
 
 // ------------------------------------------------------------------------------------------
-// Per-element codec functors.  setup(row) reads the row-uniform state; apply(x, row, j) -> C(x).
+// Exact fp32 division, fast.  For a fixed divisor b with rb = RN(1/b) (IEEE, once per row or
+// per level interval), Markstein's sequence  q0 = a*rb; r = fma(-q0, b, a) (exact);
+// q = fma(r, rb, q0)  is the correctly rounded a/b when nothing under/overflows (Markstein
+// 1990; Muller et al., Handbook of FP Arithmetic, "Markstein's theorem").  a/b of two floats is
+// never a rounding midpoint, so the tiny error of rb cannot flip a tie.  The window: divisor in
+// [2^-40, 2^80], numerator 0 or in [2^-80, 2^80] (below, r or q underflows and the identity
+// fails — measured); elsewhere the IEEE division.  The norm pass marks rows whose every element
+// is inside the window (rowfast), so their |x|/pnorm takes div_fast with no per-element guard.
+// tests/test_gpu_parity.py checks the identity exhaustively, for a set of divisors, over EVERY
+// float numerator of the window (flc_selftest_division).
 // ------------------------------------------------------------------------------------------
-struct UniformSrc {
-    const double* u;      // compat: [n][uld] float64 numpy draws; nullptr -> device RNG
-    int64_t uld;
-    uint64_t seed;
-    int64_t client0;
+struct FastDiv {
+    float b, rb;
+    bool ok;
+};
+__device__ inline FastDiv make_div(float b) {
+    FastDiv f;
+    f.b = b;
+    f.rb = 1.0f / b;
+    const float ab = fabsf(b);
+    f.ok = ab >= 0x1p-40f && ab <= 0x1p80f;   // also false for NaN
+    return f;
+}
+__device__ inline float div_fast(float a, const FastDiv& f) {   // caller guarantees the window
+    const float q0 = a * f.rb;
+    const float r = fmaf(-q0, f.b, a);
+    return fmaf(r, f.rb, q0);
+}
+__device__ inline float div_rn(float a, const FastDiv& f) {
+    const float aa = fabsf(a);
+    if (f.ok && (aa == 0.f || (aa >= 0x1p-80f && aa <= 0x1p80f))) return div_fast(a, f);
+    return a / f.b;
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-row state, computed once per row (k_norm_final / k_row_keys), read by the element loops
+// with scalar loads: the norm, its reciprocal (div_fast), the fast-window flag and the device
+// RNG row key.  Per-column state (the hashed element index) is computed once per column.
+// ------------------------------------------------------------------------------------------
+struct RowTabs {
+    const float* pn;        // [n] norm
+    const float* rpn;       // [n] RN(1/norm)
+    const uint32_t* fast;   // [n] row inside the div_fast window (nullptr: guarded path)
+    const uint32_t* rk;     // [n] device-RNG row key (nullptr in compat mode)
 };
 
+struct UniformSrc {
+    const double* u;        // compat: [n][uld] float64 numpy draws
+    int64_t uld;
+};
+
+// the reference's decision `testp < p` (float64 draw vs fp32 p promoted), compressors.py:260, 288.
+// Device mode: h = fmix32(colbase(j) ^ rowkey) against thr32 (common.hpp); p2 = p * 2^32.
+template <bool COMPAT>
+__device__ inline bool draw_below(const double* urow, uint32_t rk, int64_t j, uint32_t cs, float p, float p2) {
+    if (COMPAT) return urow[j] < (double)p;
+    uint32_t t;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(t) : "v"(ceilf(p2)));   // saturating: thr32(p)
+    return fmix32(cs ^ rk) < t;
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-element codecs.  setup(row) loads row-uniform state; col(j) is the per-column state
+// (hoisted out of the row loop); apply<F>(x, j, cs, tab) -> C(x)[j].  `tab` is the LDS level
+// table passed straight from the kernel's __shared__ array.
+// ------------------------------------------------------------------------------------------
 struct IdentOp {
+    static constexpr bool TABLE = false;
+    static constexpr bool HAS_APPLY4 = false;
     __device__ inline void setup(int64_t) {}
-    __device__ inline float apply(float x, int64_t) const { return x; }
+    __device__ inline bool row_fast() const { return false; }
+    __device__ inline void set_table_ok(bool) {}
+    __device__ inline uint32_t col(int64_t) const { return 0u; }
+    template <bool F>
+    __device__ inline float apply(float x, int64_t, uint32_t, const float4*) const { return x; }
 };
 
 struct LazyOp {                       // compressors.py:231-238: x / P if testp < P else 0
+    static constexpr bool TABLE = false;
+    static constexpr bool HAS_APPLY4 = false;
     const double* lazy_u;             // [n] float64 draws (numpy random())
     float P;
     bool keep;
     __device__ inline void setup(int64_t row) { keep = lazy_u[row] < (double)P; }
-    __device__ inline float apply(float x, int64_t) const { return keep ? x / P : 0.f; }
+    __device__ inline bool row_fast() const { return false; }
+    __device__ inline void set_table_ok(bool) {}
+    __device__ inline uint32_t col(int64_t) const { return 0u; }
+    template <bool F>
+    __device__ inline float apply(float x, int64_t, uint32_t, const float4*) const { return keep ? x / P : 0.f; }
 };
 
+template <bool COMPAT>
 struct NaturalOp {                    // compressors.py:247-268
+    static constexpr bool TABLE = false;
+    static constexpr bool HAS_APPLY4 = false;
     UniformSrc us;
+    const uint32_t* rks;
     const double* urow;
-    uint64_t ckey;
+    uint32_t rk;
     __device__ inline void setup(int64_t row) {
-        urow = us.u ? us.u + row * us.uld : nullptr;
-        ckey = client_key(us.seed, us.client0 + row);
+        urow = COMPAT ? us.u + row * us.uld : nullptr;
+        rk = COMPAT ? 0u : rks[row];
     }
-    __device__ inline float apply(float x, int64_t j) const {
+    __device__ inline bool row_fast() const { return false; }
+    __device__ inline void set_table_ok(bool) {}
+    __device__ inline uint32_t col(int64_t j) const { return COMPAT ? 0u : colbase((uint32_t)j); }
+    __device__ static inline float pow2(float e) {   // torch.pow(2, e) for integral or +-inf/NaN e
+        if (!(fabsf(e) <= 200.f)) return exp2f(e);   // inf -> inf, -inf -> 0, NaN -> NaN
+        return ldexpf(1.f, (int)e);                  // exact, incl. subnormal results and 2^128 = inf
+    }
+    template <bool F>
+    __device__ inline float apply(float x, int64_t j, uint32_t cs, const float4*) const {
         const float ax = fabsf(x);
         const float alpha = (float)log2((double)ax);          // correctly rounded fp32 log2
         const float lo = floorf(alpha), hi = ceilf(alpha);
-        const float plo = exp2f(lo), phi = exp2f(hi);         // exact for integral exponents
+        const float plo = pow2(lo), phi = pow2(hi);
         const float pt = (phi - ax) / plo;
-        const double u = urow ? urow[j] : uniform53(ckey, j);
-        const bool down = u < (double)pt;
-        float out = tsign(x) * (down ? plo : phi);
+        const bool down = draw_below<COMPAT>(urow, rk, j, cs, pt, ldexpf(pt, 32));
+        const float out = tsign(x) * (down ? plo : phi);
         return (x == 0.f) ? 0.f : out;
     }
 };
 
-// Standard / natural dithering (compressors.py:270-329).  levels in LDS as {l[s], l[s+1], l[s]-l[s+1]}.
-template <bool NATBUG>
+// Standard / natural dithering (compressors.py:270-329).  tab[g] = {l[g], l[g+1],
+// (l[g]-l[g+1]) * 2^-32, 2^32 / (l[g]-l[g+1])}: the gap is stored pre-scaled so the fast
+// division yields p * 2^32 directly (scaling by a power of two commutes with rounding).
+// NATBUG: the reference returns (y*sign)*pnorm (its line 326).
+template <bool NATBUG, bool COMPAT>
 struct DitherOp {
+    static constexpr bool TABLE = !NATBUG;
+    static constexpr bool HAS_APPLY4 = !NATBUG;
     UniformSrc us;
-    const float* pnorms;   // [n] fp32 norms
-    const float4* tab;     // LDS table, s entries
+    RowTabs rt;
     int s;
-    float pn;
+    float sf;
+    FastDiv dn;
     const double* urow;
-    uint64_t ckey;
+    uint32_t rk;
+    bool fast;
+    bool tab_ok;               // every level gap inside the div_fast window (load_table)
     __device__ inline void setup(int64_t row) {
-        pn = pnorms[row];
-        urow = us.u ? us.u + row * us.uld : nullptr;
-        ckey = client_key(us.seed, us.client0 + row);
-    }
-    __device__ inline float apply(float x, int64_t j) const {
-        const float y = fabsf(x) / pn;
-        if (NATBUG) return (y * tsign(x)) * pn;              // compressors.py:326
-        float lev = 0.f;                                      // no interval matched -> 0
-        if (y >= 0.f && y <= 1.f) {                           // levels span exactly [0, 1]
-            int g = (int)(y * (float)s);
-            g = g < 0 ? 0 : (g > s - 1 ? s - 1 : g);
-            float4 t = tab[g];
-            while (g > 0 && y < t.x) t = tab[--g];
-            while (g < s - 1 && y > t.y) t = tab[++g];
-            if (y >= t.x && y <= t.y) {
-                const float p = (y - t.y) / t.z;
-                const double u = urow ? urow[j] : uniform53(ckey, j);
-                lev = (u < (double)p) ? t.x : t.y;
-            }
+        dn.b = rt.pn[row];
+        if (rt.fast) {
+            dn.rb = rt.rpn[row];
+            dn.ok = fabsf(dn.b) >= 0x1p-40f && fabsf(dn.b) <= 0x1p80f;
+            fast = rt.fast[row] && (NATBUG || tab_ok);
+        } else {
+            dn = make_div(dn.b);
+            fast = false;
         }
-        if (x == 0.f) lev = 0.f;
-        return (lev * tsign(x)) * pn;
+        urow = COMPAT ? us.u + row * us.uld : nullptr;
+        rk = (COMPAT || NATBUG) ? 0u : rt.rk[row];
+    }
+    __device__ inline bool row_fast() const { return fast; }
+    __device__ inline void set_table_ok(bool ok) { tab_ok = ok; }
+    __device__ inline uint32_t col(int64_t j) const { return (COMPAT || NATBUG) ? 0u : colbase((uint32_t)j); }
+    template <bool F>
+    __device__ inline float apply(float x, int64_t j, uint32_t cs, const float4* tab) const {
+        // F: the row and the level table are inside the div_fast window (row_fast()); the element
+        // path is then branch-free but for the rare one-interval correction of the guess.
+        const float ax = fabsf(x);
+        const float y = F ? div_fast(ax, dn) : div_rn(ax, dn);                  // |x| / pnorm
+        if (NATBUG) return (y * tsign(x)) * dn.b;
+        int g = (int)(y * sf);                                 // y >= 0; NaN -> 0
+        g = g > s - 1 ? s - 1 : g;
+        float4 t = tab[g];
+        const bool below = y < t.x, above = y > t.y;
+        if (below | above) {                                   // std levels RN(k/s): at most one off
+            g = below ? (g > 0 ? g - 1 : 0) : (g < s - 1 ? g + 1 : g);
+            t = tab[g];
+        }
+        const bool in = y <= t.y;                              // y > 1 or NaN: no interval -> 0
+        const float num = y - t.y;
+        FastDiv dd;
+        dd.b = t.z; dd.rb = t.w; dd.ok = true;
+        const float p2 = (F || t.w != 0.f) ? div_fast(num, dd) : num / t.z;      // p * 2^32
+        const bool down = draw_below<COMPAT>(urow, rk, j, cs, COMPAT ? ldexpf(p2, -32) : 0.f, p2);
+        const float lev = in ? (down ? t.x : t.y) : 0.f;
+        // (lev * sign(x)) * pnorm with out[x == 0] = 0 (compressors.py:294-296)
+        return (x == 0.f) ? 0.f : copysignf(lev, x) * dn.b;
+    }
+    // Four elements with no per-element branch: the guessed interval is assumed right and the
+    // rare elements where it is not (y within an ulp of a level, or y > 1 / NaN) are redone by
+    // apply<F> after all four are issued — so the compiler can interleave the four chains.
+    template <bool F>
+    __device__ inline float guess_elem(float x, int64_t j, uint32_t cs, const float4* tab, bool& fix) const {
+        const float ax = fabsf(x);
+        const float y = F ? div_fast(ax, dn) : div_rn(ax, dn);
+        int g = (int)(y * sf);
+        g = g > s - 1 ? s - 1 : g;
+        const float4 t = tab[g];
+        fix = (y < t.x) | !(y <= t.y);
+        FastDiv dd;
+        dd.b = t.z; dd.rb = t.w; dd.ok = true;
+        const float num = y - t.y;
+        const float p2 = (F || t.w != 0.f) ? div_fast(num, dd) : num / t.z;
+        const bool down = draw_below<COMPAT>(urow, rk, j, cs, COMPAT ? ldexpf(p2, -32) : 0.f, p2);
+        const float lev = down ? t.x : t.y;
+        return (x == 0.f) ? 0.f : copysignf(lev, x) * dn.b;
+    }
+    template <bool F>
+    __device__ inline float4 apply4(float4 v, int64_t j, const uint32_t* cs, const float4* tab) const {
+        bool f0, f1, f2, f3;
+        float4 r = make_float4(guess_elem<F>(v.x, j, cs[0], tab, f0), guess_elem<F>(v.y, j + 1, cs[1], tab, f1),
+                               guess_elem<F>(v.z, j + 2, cs[2], tab, f2), guess_elem<F>(v.w, j + 3, cs[3], tab, f3));
+        if (f0 | f1 | f2 | f3) {
+            if (f0) r.x = apply<F>(v.x, j, cs[0], tab);
+            if (f1) r.y = apply<F>(v.y, j + 1, cs[1], tab);
+            if (f2) r.z = apply<F>(v.z, j + 2, cs[2], tab);
+            if (f3) r.w = apply<F>(v.w, j + 3, cs[3], tab);
+        }
+        return r;
     }
 };
 
-// Natural-dithering levels are not uniform: the (int)(y*s) guess is then refined by the loops
-// above; with levels 2^-k the walk is bounded by s.  A binary search would be shorter for large
-// s; s <= 32 in practice (nat.dithering:10 in the reference's GUI list).
+template <bool F, class Op>
+__device__ inline float4 apply4(const Op& op, float4 v, int64_t j, const uint32_t* cs, const float4* tab) {
+    if constexpr (Op::HAS_APPLY4) {
+        return op.template apply4<F>(v, j, cs, tab);
+    } else {
+        return make_float4(op.template apply<F>(v.x, j, cs[0], tab), op.template apply<F>(v.y, j + 1, cs[1], tab),
+                           op.template apply<F>(v.z, j + 2, cs[2], tab), op.template apply<F>(v.w, j + 3, cs[3], tab));
+    }
+}
 
-template <class Op>
-__device__ inline float4 apply4(const Op& op, float4 v, int64_t j) {
-    return make_float4(op.apply(v.x, j), op.apply(v.y, j + 1), op.apply(v.z, j + 2), op.apply(v.w, j + 3));
+// level table (see DitherOp); returns (block-uniform) whether every gap is inside the window
+__device__ inline bool load_table(const float* levels, int s, float4* tab) {
+    int bad = 0;
+    for (int i = threadIdx.x; i < s; i += blockDim.x) {
+        const float lo = levels[i], hi = levels[i + 1], den = lo - hi;
+        const float ad = fabsf(den);
+        // div_fast window: gap in [2^-40, 2^80] and every nonzero y - hi >= ulp(hi) >= 2^-80
+        const bool ok = ad >= 0x1p-40f && ad <= 0x1p80f && hi >= 0x1p-56f;
+        const float sden = ldexpf(den, -32);
+        tab[i] = make_float4(lo, hi, sden, ok ? 1.0f / sden : 0.f);
+        bad |= !ok;
+    }
+    return __syncthreads_or(bad) == 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -197,126 +386,126 @@ __device__ inline float4 apply4(const Op& op, float4 v, int64_t j) {
 // ------------------------------------------------------------------------------------------
 template <class Op, bool VEC>
 __global__ __launch_bounds__(256) void k_ew_dense(const float* __restrict__ x, int64_t d, Op op,
-                                                  const float* __restrict__ levels, float* __restrict__ out) {
+                                                  const float* __restrict__ levels, int s, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem_tab[];
-    if (levels) {   // dithering table
-        int s = op.s_for_table();
-        for (int i = threadIdx.x; i < s; i += blockDim.x)
-            smem_tab[i] = make_float4(levels[i], levels[i + 1], levels[i] - levels[i + 1], 0.f);
-        __syncthreads();
-        op.bind_table(smem_tab);
-    }
+    if (Op::TABLE) op.set_table_ok(load_table(levels, s, smem_tab));
     op.setup(0);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t j0 = VEC ? (d / 4) * 4 : 0;
     if (VEC) {
-        const int64_t groups = d / 4;
-        for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride)
-            reinterpret_cast<float4*>(out)[g] = apply4(op, reinterpret_cast<const float4*>(x)[g], g * 4);
-        for (int64_t j = groups * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
-            out[j] = op.apply(x[j], j);
-    } else {
-        for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
-            out[j] = op.apply(x[j], j);
+        for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < d / 4; g += stride) {
+            uint32_t cs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cs[q] = op.col(g * 4 + q);
+            const float4 v = reinterpret_cast<const float4*>(x)[g];
+            reinterpret_cast<float4*>(out)[g] = op.row_fast() ? apply4<true>(op, v, g * 4, cs, smem_tab)
+                                                              : apply4<false>(op, v, g * 4, cs, smem_tab);
+        }
     }
+    for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
+        out[j] = op.template apply<false>(x[j], j, op.col(j), smem_tab);
 }
 
 // ------------------------------------------------------------------------------------------
-// Fused encode + reduce over N rows (tile owner, rows folded in order).
+// Fused encode + reduce over N rows.  Tile owner: a thread owns COLS float4 column groups for
+// the whole launch and folds rows 0..N-1 into registers in order; PF rows are in flight
+// (a register ring with static indices), so each lane keeps PF*COLS*16 B of loads outstanding.
 // ------------------------------------------------------------------------------------------
-template <class Op, int COLS>
+template <class Op, int COLS, int PF, bool W>
 __global__ __launch_bounds__(256) void k_ew_accum_vec(RowSrc src, int64_t n, int64_t d, Op op,
-                                                      const float* __restrict__ levels,
+                                                      const float* __restrict__ levels, int s,
                                                       const float* __restrict__ w, float wt,
                                                       float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem_tab[];
-    if (levels) {
-        int s = op.s_for_table();
-        for (int i = threadIdx.x; i < s; i += blockDim.x)
-            smem_tab[i] = make_float4(levels[i], levels[i + 1], levels[i] - levels[i + 1], 0.f);
-        __syncthreads();
-        op.bind_table(smem_tab);
-    }
+    if (Op::TABLE) op.set_table_ok(load_table(levels, s, smem_tab));
     const int64_t groups = d / 4;
     const int64_t tile_groups = (int64_t)blockDim.x * COLS;
     for (int64_t t0 = (int64_t)blockIdx.x * tile_groups; t0 < groups; t0 += (int64_t)gridDim.x * tile_groups) {
-        // thread's column groups: t0 + threadIdx.x + c*256 (coalesced per c)
-        float4 acc[COLS];
-        float4 cur[COLS];
+        int64_t gi[COLS];
         bool ok[COLS];
+        uint32_t cs[COLS][4];
 #pragma unroll
-        for (int c = 0; c < COLS; ++c) ok[c] = (t0 + threadIdx.x + c * 256) < groups;
-        {
-            const float4* r0 = reinterpret_cast<const float4*>(src.row(0));
+        for (int c = 0; c < COLS; ++c) {
+            gi[c] = t0 + threadIdx.x + c * 256;
+            ok[c] = gi[c] < groups;
 #pragma unroll
-            for (int c = 0; c < COLS; ++c) cur[c] = ok[c] ? r0[t0 + threadIdx.x + c * 256] : make_float4(0, 0, 0, 0);
+            for (int q = 0; q < 4; ++q) cs[c][q] = op.col(gi[c] * 4 + q);
         }
-        for (int64_t i = 0; i < n; ++i) {
-            float4 nxt[COLS];
-            if (i + 1 < n) {
-                const float4* rn = reinterpret_cast<const float4*>(src.row(i + 1));
+        float4 ring[PF][COLS];
 #pragma unroll
-                for (int c = 0; c < COLS; ++c) nxt[c] = ok[c] ? rn[t0 + threadIdx.x + c * 256] : make_float4(0, 0, 0, 0);
+        for (int p = 0; p < PF; ++p) {
+            if (p < n) {
+                const float4* r = reinterpret_cast<const float4*>(src.row(p));
+#pragma unroll
+                for (int c = 0; c < COLS; ++c) ring[p][c] = ok[c] ? r[gi[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            op.setup(i);
-            const float wi = w ? w[i] : 1.f;
+        }
+        float4 acc[COLS];
+        for (int64_t i0 = 0; i0 < n; i0 += PF) {
 #pragma unroll
-            for (int c = 0; c < COLS; ++c) {
-                const int64_t j = (t0 + threadIdx.x + c * 256) * 4;
-                float4 e = apply4(op, cur[c], j);
-                float4 t = make_float4(wi * e.x, wi * e.y, wi * e.z, wi * e.w);
-                if (i == 0) acc[c] = t;
-                else { acc[c].x = acc[c].x + t.x; acc[c].y = acc[c].y + t.y; acc[c].z = acc[c].z + t.z; acc[c].w = acc[c].w + t.w; }
-            }
-            if (i + 1 < n) {
+            for (int p = 0; p < PF; ++p) {
+                const int64_t i = i0 + p;
+                if (i < n) {
+                    op.setup(i);
+                    const float wi = W ? w[i] : 1.f;
+                    float4 e[COLS];
+                    if (op.row_fast()) {   // row-uniform: whole row inside the fast-division window
 #pragma unroll
-                for (int c = 0; c < COLS; ++c) cur[c] = nxt[c];
+                        for (int c = 0; c < COLS; ++c) e[c] = apply4<true>(op, ring[p][c], gi[c] * 4, cs[c], smem_tab);
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < COLS; ++c) e[c] = apply4<false>(op, ring[p][c], gi[c] * 4, cs[c], smem_tab);
+                    }
+#pragma unroll
+                    for (int c = 0; c < COLS; ++c) {
+                        const float4 t = W ? make_float4(wi * e[c].x, wi * e[c].y, wi * e[c].z, wi * e[c].w) : e[c];
+                        if (i == 0) acc[c] = t;
+                        else {
+                            acc[c].x = acc[c].x + t.x; acc[c].y = acc[c].y + t.y;
+                            acc[c].z = acc[c].z + t.z; acc[c].w = acc[c].w + t.w;
+                        }
+                    }
+                    if (i + PF < n) {
+                        const float4* r = reinterpret_cast<const float4*>(src.row(i + PF));
+#pragma unroll
+                        for (int c = 0; c < COLS; ++c) ring[p][c] = ok[c] ? r[gi[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
             }
         }
 #pragma unroll
         for (int c = 0; c < COLS; ++c)
             if (ok[c])
-                reinterpret_cast<float4*>(out)[t0 + threadIdx.x + c * 256] =
+                reinterpret_cast<float4*>(out)[gi[c]] =
                     make_float4(acc[c].x / wt, acc[c].y / wt, acc[c].z / wt, acc[c].w / wt);
     }
 }
 
 template <class Op>
 __global__ __launch_bounds__(256) void k_ew_accum_scalar(RowSrc src, int64_t n, int64_t j0, int64_t d, Op op,
-                                                         const float* __restrict__ levels,
+                                                         const float* __restrict__ levels, int s,
                                                          const float* __restrict__ w, float wt,
                                                          float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem_tab[];
-    if (levels) {
-        int s = op.s_for_table();
-        for (int i = threadIdx.x; i < s; i += blockDim.x)
-            smem_tab[i] = make_float4(levels[i], levels[i + 1], levels[i] - levels[i + 1], 0.f);
-        __syncthreads();
-        op.bind_table(smem_tab);
-    }
+    if (Op::TABLE) op.set_table_ok(load_table(levels, s, smem_tab));
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride) {
+        const uint32_t cs = op.col(j);
         float acc = 0.f;
         for (int64_t i = 0; i < n; ++i) {
             op.setup(i);
-            float t = (w ? w[i] : 1.f) * op.apply(src.row(i)[j], j);
+            const float t = (w ? w[i] : 1.f) * op.template apply<false>(src.row(i)[j], j, cs, smem_tab);
             acc = (i == 0) ? t : acc + t;
         }
         out[j] = acc / wt;
     }
 }
 
-// Table plumbing for the functors (only dithering uses it).
-template <class Base>
-struct WithTable : Base {
-    int s_tab = 0;
-    __device__ inline int s_for_table() const { return s_tab; }
-    __device__ inline void bind_table(const float4*) {}
-};
-template <bool NB>
-struct DitherT : DitherOp<NB> {
-    __device__ inline int s_for_table() const { return this->s; }
-    __device__ inline void bind_table(const float4* t) { this->tab = t; }
-};
+// device-RNG row keys (natural codec; dithering gets them from k_norm_final)
+__global__ void k_row_keys(int64_t n, uint64_t seed, int64_t client0, uint32_t* __restrict__ rk) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        rk[r] = rowkey(client_key(seed, client0 + r));
+}
 
 static int grid_cap(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;
@@ -327,11 +516,40 @@ template <class Op>
 static int launch_dense(const float* x, int64_t d, Op op, const float* levels, int s, float* out, hipStream_t st) {
     if (d == 0) return FLC_OK;
     const bool vec = (((uintptr_t)x | (uintptr_t)out) & 15u) == 0;
-    size_t lds = levels ? (size_t)s * sizeof(float4) : 0;
-    int grid = grid_cap(vec ? (d + 3) / 4 : d, 256, 4096);
-    if (vec) hipLaunchKernelGGL((k_ew_dense<Op, true>), dim3(grid), dim3(256), lds, st, x, d, op, levels, out);
-    else hipLaunchKernelGGL((k_ew_dense<Op, false>), dim3(grid), dim3(256), lds, st, x, d, op, levels, out);
+    const size_t lds = Op::TABLE ? (size_t)s * sizeof(float4) : 0;
+    const int grid = grid_cap(vec ? (d + 3) / 4 : d, 256, 4096);
+    if (vec) hipLaunchKernelGGL((k_ew_dense<Op, true>), dim3(grid), dim3(256), lds, st, x, d, op, levels, s, out);
+    else hipLaunchKernelGGL((k_ew_dense<Op, false>), dim3(grid), dim3(256), lds, st, x, d, op, levels, s, out);
     FLC_CHECK_LAUNCH("k_ew_dense");
+    return FLC_OK;
+}
+
+// tile shape of the accumulate kernel: COLS float4 columns per thread, PF rows in flight;
+// FLC_EW_TILE=<cols>x<pf> overrides (tuning runs only).
+static int ew_tile_variant() {
+    static int v = [] {
+        const char* e = getenv("FLC_EW_TILE");
+        if (!e) return 0;
+        if (!strcmp(e, "2x2")) return 1;
+        if (!strcmp(e, "2x4")) return 2;
+        if (!strcmp(e, "1x8")) return 3;
+        if (!strcmp(e, "1x4")) return 4;
+        if (!strcmp(e, "4x2")) return 5;
+        return 0;
+    }();
+    return v;
+}
+
+template <class Op, int COLS, int PF>
+static int launch_accum_tile(RowSrc src, int64_t n, int64_t d, Op op, const float* levels, int s, const float* w,
+                             float wt, float* out, size_t lds, hipStream_t st) {
+    const int64_t groups = d / 4;
+    const int grid = grid_cap(groups, 256 * COLS, 1 << 20);
+    ProfScope _ps("k_ew_accum_vec", st);
+    if (w) hipLaunchKernelGGL((k_ew_accum_vec<Op, COLS, PF, true>), dim3(grid), dim3(256), lds, st, src, n, d, op,
+                              levels, s, w, wt, out);
+    else hipLaunchKernelGGL((k_ew_accum_vec<Op, COLS, PF, false>), dim3(grid), dim3(256), lds, st, src, n, d, op,
+                            levels, s, w, wt, out);
     return FLC_OK;
 }
 
@@ -339,24 +557,25 @@ template <class Op>
 static int launch_accum(RowSrc src, bool vec, int64_t n, int64_t d, Op op, const float* levels, int s,
                         const float* w, float wt, float* out, hipStream_t st) {
     if (d == 0) return FLC_OK;
-    size_t lds = levels ? (size_t)s * sizeof(float4) : 0;
+    const size_t lds = Op::TABLE ? (size_t)s * sizeof(float4) : 0;
     int64_t j0 = 0;
     if (vec && ((uintptr_t)out & 15u) == 0) {
-        constexpr int COLS = 4;
-        const int64_t groups = d / 4;
-        if (groups > 0) {
-            int grid = grid_cap(groups, 256 * COLS, 1 << 20);
-{ ProfScope _ps("k_ew_accum_vec", st);
-            hipLaunchKernelGGL((k_ew_accum_vec<Op, COLS>), dim3(grid), dim3(256), lds, st, src, n, d, op, levels, w,
-                               wt, out); }
+        if (d / 4 > 0) {
+            switch (ew_tile_variant()) {
+                case 1: launch_accum_tile<Op, 2, 2>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+                case 3: launch_accum_tile<Op, 1, 8>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+                case 4: launch_accum_tile<Op, 1, 4>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+                case 5: launch_accum_tile<Op, 4, 2>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+                default: launch_accum_tile<Op, 2, 4>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+            }
             FLC_CHECK_LAUNCH("k_ew_accum_vec");
         }
-        j0 = groups * 4;
+        j0 = (d / 4) * 4;
     }
     if (j0 < d) {
-        int grid = grid_cap(d - j0, 256, 4096);
-        hipLaunchKernelGGL((k_ew_accum_scalar<Op>), dim3(grid), dim3(256), lds, st, src, n, j0, d, op, levels, w, wt,
-                           out);
+        const int grid = grid_cap(d - j0, 256, 4096);
+        hipLaunchKernelGGL((k_ew_accum_scalar<Op>), dim3(grid), dim3(256), lds, st, src, n, j0, d, op, levels, s, w,
+                           wt, out);
         FLC_CHECK_LAUNCH("k_ew_accum_scalar");
     }
     return FLC_OK;
@@ -365,13 +584,33 @@ static int launch_accum(RowSrc src, bool vec, int64_t n, int64_t d, Op op, const
 // ------------------------------------------------------------------------------------------
 // Entry points used by api.hip
 // ------------------------------------------------------------------------------------------
+struct EwWs {
+    double* partial;
+    uint32_t* tinyp;
+    float* pn;
+    float* rpn;
+    uint32_t* fast;
+    uint32_t* rk;
+};
+static EwWs carve_ew(void* base, int64_t n, int64_t d, size_t* bytes) {
+    Carver c(base);
+    const size_t np = (size_t)std::max<int64_t>(n, 1), parts = (size_t)std::max<int64_t>(norm_parts(d), 1);
+    EwWs w;
+    w.partial = c.take<double>(np * parts);
+    w.tinyp = c.take<uint32_t>(np * parts);
+    w.pn = c.take<float>(np);
+    w.rpn = c.take<float>(np);
+    w.fast = c.take<uint32_t>(np);
+    w.rk = c.take<uint32_t>(np);
+    if (bytes) *bytes = c.bytes();
+    return w;
+}
+
 size_t ew_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
-    Carver c(nullptr);
-    if (prm->codec == FLC_STD_DITHERING || prm->codec == FLC_NAT_DITHERING) {
-        c.take<double>((size_t)std::max<int64_t>(n, 1) * std::max<int64_t>(norm_parts(d), 1));
-        c.take<float>((size_t)std::max<int64_t>(n, 1));
-    }
-    return c.bytes();
+    if (prm->codec == FLC_IDENT || prm->codec == FLC_LAZY) return 0;
+    size_t b = 0;
+    carve_ew(nullptr, n, d, &b);
+    return b;
 }
 
 static int check_dither(const flc_codec_params* prm) {
@@ -389,58 +628,98 @@ int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool
            const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt,
            void* ws, size_t ws_bytes, hipStream_t st) {
     const int codec = prm->codec;
-    UniformSrc us{pat ? pat->d_uniforms : nullptr, (pat && pat->uniforms_ld) ? pat->uniforms_ld : d,
-                  prm->seed, pat ? pat->client0 : 0};
+    const bool compat = pat && pat->d_uniforms;
+    const int64_t client0 = pat ? pat->client0 : 0;
+    UniformSrc us{compat ? pat->d_uniforms : nullptr, (pat && pat->uniforms_ld) ? pat->uniforms_ld : d};
     auto go = [&](auto op, const float* levels, int s) -> int {
         if (dense) return launch_dense(src.base, d, op, levels, s, out, st);
         return launch_accum(src, vec, n, d, op, levels, s, w, wt, out, st);
     };
+    if (ws_bytes < ew_workspace(prm, n, d)) { set_error("codec workspace too small"); return FLC_ERR_WORKSPACE; }
+    EwWs e = carve_ew(ws, n, d, nullptr);
     switch (codec) {
         case FLC_IDENT: {
-            WithTable<IdentOp> op;
+            IdentOp op;
             return go(op, nullptr, 0);
         }
         case FLC_LAZY: {
             if (!pat || !pat->d_lazy_u) { set_error("lazy: pattern needs d_lazy_u"); return FLC_ERR_ARG; }
-            WithTable<LazyOp> op;
+            LazyOp op;
             op.lazy_u = pat->d_lazy_u;
             op.P = prm->lazy_p;
             return go(op, nullptr, 0);
         }
         case FLC_NATURAL: {
-            WithTable<NaturalOp> op;
+            if (compat) { NaturalOp<true> op; op.us = us; op.rks = nullptr; return go(op, nullptr, 0); }
+            hipLaunchKernelGGL(k_row_keys, dim3(grid_cap(n, 256, 64)), dim3(256), 0, st, n, prm->seed, client0, e.rk);
+            FLC_CHECK_LAUNCH("k_row_keys");
+            NaturalOp<false> op;
             op.us = us;
+            op.rks = e.rk;
             return go(op, nullptr, 0);
         }
         case FLC_STD_DITHERING:
         case FLC_NAT_DITHERING: {
             int rc = check_dither(prm);
             if (rc) return rc;
-            if (ws_bytes < ew_workspace(prm, n, d)) { set_error("dithering: workspace too small"); return FLC_ERR_WORKSPACE; }
-            Carver c(ws);
-            double* partial = c.take<double>((size_t)std::max<int64_t>(n, 1) * std::max<int64_t>(norm_parts(d), 1));
-            float* pn = c.take<float>((size_t)std::max<int64_t>(n, 1));
-            const float* pn_use = pnorm_in;
-            if (!pn_use) {
-                rc = launch_norms(src, vec, n, d, prm->norm, partial, pn, st);
+            RowTabs rt{pnorm_in, nullptr, nullptr, e.rk};
+            if (!pnorm_in) {
+                rc = launch_norms(src, vec, n, d, prm->norm, e.partial, e.tinyp, e.pn, e.rpn, e.fast, prm->seed,
+                                  client0, e.rk, st);
                 if (rc) return rc;
-                pn_use = pn;
+                rt = RowTabs{e.pn, e.rpn, e.fast, e.rk};
+            } else if (!compat) {
+                hipLaunchKernelGGL(k_row_keys, dim3(grid_cap(n, 256, 64)), dim3(256), 0, st, n, prm->seed, client0, e.rk);
+                FLC_CHECK_LAUNCH("k_row_keys");
             }
-            if (pnorm_out && pnorm_out != pn_use)
-                FLC_CHECK_HIP(hipMemcpyAsync(pnorm_out, pn_use, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, st));
+            if (pnorm_out && pnorm_out != rt.pn)
+                FLC_CHECK_HIP(hipMemcpyAsync(pnorm_out, rt.pn, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, st));
+            auto fill = [&](auto& op) {
+                op.us = us; op.rt = rt; op.s = prm->s; op.sf = (float)prm->s; op.tab_ok = false;
+            };
             if (codec == FLC_STD_DITHERING) {
-                DitherT<false> op;
-                op.us = us; op.pnorms = pn_use; op.s = prm->s; op.tab = nullptr;
+                if (compat) { DitherOp<false, true> op; fill(op); return go(op, prm->d_levels, prm->s); }
+                DitherOp<false, false> op;
+                fill(op);
                 return go(op, prm->d_levels, prm->s);
             }
-            DitherT<true> op;
-            op.us = us; op.pnorms = pn_use; op.s = prm->s; op.tab = nullptr;
+            DitherOp<true, false> op;   // natural dithering output does not depend on the draws
+            fill(op);
             return go(op, prm->d_levels, prm->s);
         }
         default:
             set_error("ew_run: codec %d is not elementwise", codec);
             return FLC_ERR_UNSUPPORTED;
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Self-test of the fast division: for each divisor, every float numerator in [2^-80, 2^80] (the
+// window div_rn / div_fast use) is divided both ways; mismatches are counted.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_selftest_div(const float* __restrict__ bs, int nb,
+                                                      unsigned long long* __restrict__ bad) {
+    const uint32_t lo = __float_as_uint(0x1p-80f), hi = __float_as_uint(0x1p80f);
+    const uint64_t count = (uint64_t)(hi - lo) + 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < nb; ++k) {
+        const FastDiv f = make_div(bs[k]);
+        unsigned long long local = 0;
+        for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
+            const float a = __uint_as_float(lo + (uint32_t)t);
+            const float q = div_rn(a, f), r = a / f.b;
+            local += (__float_as_uint(q) != __float_as_uint(r)) ? 1ull : 0ull;
+        }
+        local = wave_sum(local);
+        if ((threadIdx.x & 63) == 0 && local) atomicAdd(&bad[k], local);
+    }
+}
+
+int selftest_division(const float* d_b, int nb, unsigned long long* d_bad, hipStream_t st) {
+    FLC_CHECK_HIP(hipMemsetAsync(d_bad, 0, (size_t)nb * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_selftest_div, dim3(8192), dim3(256), 0, st, d_b, nb, d_bad);
+    FLC_CHECK_LAUNCH("k_selftest_div");
+    return FLC_OK;
 }
 
 }  // namespace flc

@@ -99,6 +99,41 @@ __host__ __device__ inline double uniform53(uint64_t ckey, int64_t j) {
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
 
+// Per-element device draw used by the dithering / natural kernels: a 32-bit uniform
+// u = fmix32(j * m_c + o_c) * 2^-32, with (m_c odd, o_c) taken from the client key — one Weyl
+// sequence per client through the MurmurHash3 finaliser (a bijection with full avalanche).
+// 32-bit multiplies only: the 64-bit mix above costs ~3x the VALU time per element.
+__host__ __device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+// u(client, j) = fmix32(colbase(j) ^ rowkey(client)): the column base is a fixed hash of the
+// element index (computed once per column by the kernels, outside the client loop), the row key
+// a 32-bit fold of the client key; the outer fmix32 fully avalanches their xor.
+__host__ __device__ inline uint32_t colbase(uint32_t j) { return fmix32(j * 0x9E3779B1u + 0x7F4A7C15u); }
+__host__ __device__ inline uint32_t rowkey(uint64_t ckey) { return (uint32_t)(ckey >> 32) ^ (uint32_t)ckey; }
+__host__ __device__ inline uint32_t dev_u32(uint64_t ckey, uint32_t j) { return fmix32(colbase(j) ^ rowkey(ckey)); }
+// Decision for a draw h (u = h * 2^-32) against an fp32 probability p:  h < sat_u32(ceil(p*2^32)).
+// Equals (u < p) exactly for p in [0, 1); p >= 1 admits every h but 0xFFFFFFFF (prob. 2^-32), and
+// p <= 0 or NaN admits none.  ldexp / ceil / saturating convert are exact single instructions.
+__host__ __device__ inline uint32_t thr32(float p) {
+    const float t = ceilf(ldexpf(p, 32));
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;   // v_cvt_u32_f32 saturates: < 0 -> 0, >= 2^32 -> 0xFFFFFFFF, NaN -> 0
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+#else
+    if (!(t > 0.f)) return 0u;                    // p <= 0 or NaN
+    if (t >= 4294967295.f) return 0xFFFFFFFFu;
+    return (uint32_t)t;
+#endif
+}
+__host__ __device__ inline bool below32(uint32_t h, float p) { return h < thr32(p); }
+
 // Keyed bijection on [0, d): balanced Feistel on 2h bits (4^h >= d) with cycle walking.
 // RandK device mode takes the first K images: K distinct indices drawn uniformly.
 struct Feistel {

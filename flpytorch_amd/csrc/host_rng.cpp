@@ -118,7 +118,7 @@ extern "C" int flc_mt_randint31(uint32_t* h_key, int32_t* h_pos, int64_t count, 
 }
 
 extern "C" double flc_device_uniform(uint64_t seed, int64_t client, int64_t j) {
-    return flc::uniform53(flc::client_key(seed, client), j);
+    return (double)flc::dev_u32(flc::client_key(seed, client), (uint32_t)j) * (1.0 / 4294967296.0);
 }
 
 extern "C" int flc_device_randk_indices(uint64_t seed, int64_t client, int64_t d, int64_t k, int64_t* h_out) {

@@ -280,6 +280,96 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
 }
 
 // ------------------------------------------------------------------------------------------
+// Fast-path filter: one wave per 4096-element chunk, grid-stride over (row, chunk).  The chunk
+// streams in 4 stages of 1 KB per lane-group with the next stage's loads in flight; entries
+// with key >= T_lo are compacted (ballot / mbcnt) into a wave-private LDS staging buffer, then
+// one atomic reserves the row-buffer space and the staging is copied out coalesced.  Register
+// footprint stays small so 8 waves per SIMD keep the HBM pipe full.
+// ------------------------------------------------------------------------------------------
+constexpr int STCAP = 512;           // staged entries per chunk (12.5 %; more -> row overflow)
+
+template <bool VEC>
+__device__ inline void load_stage(const float* r, int64_t j0, int sg, int lane, int64_t d, float4 (&v)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t j = j0 + (int64_t)((sg * 4 + u) * 64 + lane) * 4;
+        if (VEC && j + 3 < d) {
+            v[u] = *reinterpret_cast<const float4*>(r + j);
+        } else {
+            v[u].x = (j < d) ? r[j] : 0.f;
+            v[u].y = (j + 1 < d) ? r[j + 1] : 0.f;
+            v[u].z = (j + 2 < d) ? r[j + 2] : 0.f;
+            v[u].w = (j + 3 < d) ? r[j + 3] : 0.f;
+        }
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
+    __shared__ uint32_t st_idx[4][STCAP];
+    __shared__ float st_val[4][STCAP];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t C = nchunks(d);
+    const int64_t items = n * C;
+    uint32_t* si = st_idx[wv];
+    float* sv = st_val[wv];
+    for (int64_t it = (int64_t)blockIdx.x * 4 + wv; it < items; it += (int64_t)gridDim.x * 4) {
+        const int64_t row = it / C, c = it - row * C;
+        if (ws.flags[row]) continue;                       // row already failed (wave-uniform)
+        const float* r = rows.row(row);
+        const uint32_t T = ws.thr[row];
+        const int64_t j0 = c * CHUNK;
+        uint32_t cnt = 0;
+        float4 cur[4], nxt[4];
+        load_stage<VEC>(r, j0, 0, lane, d, cur);
+#pragma unroll
+        for (int sg = 0; sg < 4; ++sg) {
+            if (sg < 3) load_stage<VEC>(r, j0, sg + 1, lane, d, nxt);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t j = j0 + (int64_t)((sg * 4 + u) * 64 + lane) * 4;
+                const float vq[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+                const int any = (int)(mag_key(vq[0]) >= T) | (int)(mag_key(vq[1]) >= T) |
+                                (int)(mag_key(vq[2]) >= T) | (int)(mag_key(vq[3]) >= T);
+                if (__ballot(any)) {                      // ~1-2 % of elements: most groups skip
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const bool f = (j + q < d) && mag_key(vq[q]) >= T;
+                        const uint64_t m = __ballot(f);
+                        const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                        if (f && pos < STCAP) { si[pos] = (uint32_t)(j + q); sv[pos] = vq[q]; }
+                        cnt += (uint32_t)__popcll(m);
+                    }
+                }
+            }
+            if (sg < 3) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+            }
+        }
+        bool fits = cnt <= STCAP;
+        uint32_t base = 0;
+        if (fits && cnt) {
+            if (lane == 0) base = atomicAdd(&ws.rowcnt[row], cnt);
+            base = __shfl(base, 0, WAVE);
+            fits = (int64_t)base + cnt <= ws.cap;
+        }
+        if (lane == 0) {
+            ws.tab[c * n + row] = make_uint2(base, fits ? cnt : 0u);
+            if (!fits) atomicOr(&ws.flags[row], F_OVERFLOW);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // staging writes -> reads (same wave)
+        if (fits) {
+            uint32_t* oi = ws.ent_idx + row * ws.cap + base;
+            float* ov = ws.ent_val + row * ws.cap + base;
+            for (uint32_t e = lane; e < cnt; e += 64) { oi[e] = si[e]; ov[e] = sv[e]; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // reads done before the next chunk's writes
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Radix passes over candidate lists (fast path) or full rows (exact path)
 // ------------------------------------------------------------------------------------------
 // Histogram of pass p over row data; grid-stride over (row, block of 64 K elements).
@@ -358,7 +448,7 @@ __global__ void k_build_worklist(int64_t n, int64_t K, int64_t d, SelWs ws, int 
     __syncthreads();
     for (int64_t row = threadIdx.x; row < n; row += blockDim.x) {
         uint32_t f = ws.flags[row];
-        if (force_all || f) {
+        if (force_all || (f & (F_OVERFLOW | F_SHORT))) {   // ambiguous ties stay on the fast path
             uint32_t pos = atomicAdd(&cnt, 1u);
             ws.worklist[pos] = (uint32_t)row;
             ws.flags[row] = F_EXACT;
@@ -393,18 +483,55 @@ __global__ __launch_bounds__(256) void k_tie_count(RowSrc rows, int64_t n, int64
     }
 }
 
-__global__ __launch_bounds__(64) void k_tie_scan(int64_t n, int64_t d, SelWs ws) {
+// Fast path, ambiguous ties: per chunk count of key == thr in the chunk's candidate list.
+__global__ __launch_bounds__(256) void k_cand_tie_count(int64_t n, int64_t d, SelWs ws) {
     const int64_t C = nchunks(d);
-    const int64_t nrows = *ws.nwork;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t bpr = (C + 3) / 4;
+    for (int64_t it = blockIdx.x; it < n * bpr; it += gridDim.x) {
+        const int64_t row = it / bpr;
+        if ((ws.flags[row] & (F_TIES | F_EXACT)) != F_TIES) continue;
+        const int64_t c = (it % bpr) * 4 + wv;
+        if (c >= C) continue;
+        const uint2 te = ws.tab[c * n + row];
+        const uint32_t T = ws.thr[row];
+        uint32_t cnt = 0;
+        for (uint32_t e = lane; e < te.y; e += 64) cnt += (mag_key(ws.ent_val[row * ws.cap + te.x + e]) == T) ? 1u : 0u;
+        cnt = wave_sum(cnt);
+        if (lane == 0) ws.tieprefix[c * n + row] = cnt;
+    }
+}
+
+// Exclusive prefix of the per-chunk tie counts, in chunk (= index) order, for the rows that
+// need it: EXACT=false -> fast-path rows with ambiguous ties, true -> the exact-path worklist.
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_tie_scan(int64_t n, int64_t d, SelWs ws) {
+    __shared__ uint32_t part[256];
+    const int64_t C = nchunks(d);
+    const int64_t nrows = EXACT ? (int64_t)(*ws.nwork) : n;
+    const int t = threadIdx.x;
+    const int64_t per = (C + 255) / 256;           // chunks per thread (contiguous)
     for (int64_t li = blockIdx.x; li < nrows; li += gridDim.x) {
-        const int64_t row = ws.worklist[li];
-        if (threadIdx.x != 0) continue;
-        uint32_t run = 0;
-        for (int64_t c = 0; c < C; ++c) {
-            uint32_t v = ws.tieprefix[c * n + row];
+        const int64_t row = EXACT ? (int64_t)ws.worklist[li] : li;
+        if (!EXACT && (ws.flags[row] & (F_TIES | F_EXACT)) != F_TIES) continue;
+        const int64_t c0 = t * per, c1 = min(C, c0 + per);
+        uint32_t sum = 0;
+        for (int64_t c = c0; c < c1; ++c) sum += ws.tieprefix[c * n + row];
+        part[t] = sum;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            const uint32_t v = (t >= off) ? part[t - off] : 0u;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
+        }
+        uint32_t run = part[t] - sum;              // exclusive
+        for (int64_t c = c0; c < c1; ++c) {
+            const uint32_t v = ws.tieprefix[c * n + row];
             ws.tieprefix[c * n + row] = run;
             run += v;
         }
+        __syncthreads();
     }
 }
 
@@ -460,6 +587,19 @@ __global__ __launch_bounds__(256) void k_randk_scatter(RowSrc rows, int64_t n, i
 // ASSIGN (single row, no weights): out = tile with the entry values stored, not added
 // (keeps -0.0 like torch's out[ind] = x[ind]).
 // ------------------------------------------------------------------------------------------
+// Tie admission on the fast path (row flag F_TIES without F_EXACT): among the entries whose key
+// equals the K-th magnitude T, only the `need` lowest indices are summed.  rank = ties in the
+// row's earlier chunks (tieprefix) + ties of this chunk's list with a smaller index.  Taken only
+// for key == T entries of such rows (a handful per row).
+__device__ inline bool tie_admitted(const SelWs& ws, int64_t row, int64_t c, int64_t n, uint32_t off, uint32_t cnt,
+                                    uint32_t T, uint32_t idx) {
+    uint32_t rank = ws.tieprefix[c * n + row];
+    const uint32_t* li = ws.ent_idx + row * ws.cap + off;
+    const float* lv = ws.ent_val + row * ws.cap + off;
+    for (uint32_t e = 0; e < cnt; ++e) rank += (mag_key(lv[e]) == T && li[e] < idx) ? 1u : 0u;
+    return rank < ws.krem[row];
+}
+
 template <bool ASSIGN>
 __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
                                                      float wt, float* __restrict__ out) {
@@ -471,55 +611,58 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
     for (int64_t c = (int64_t)blockIdx.x * 4 + wv; c < C; c += (int64_t)gridDim.x * 4) {
         // waves are independent: each owns its tile, LDS ops of one wave retire in order
         for (int i = lane; i < CHUNK; i += 64) tl[i] = 0.f;
-        {
-            const int64_t cbase = c * CHUNK;
-            for (int64_t i0 = 0; i0 < n; i0 += PF) {
-                // lanes 0..PF-1 fetch the table entries of rows i0..i0+PF-1
-                uint2 te = make_uint2(0, 0);
-                uint32_t tthr = 0;
-                float tw = 1.f;
-                if (lane < PF && i0 + lane < n) {
-                    te = ws.tab[c * n + i0 + lane];
-                    tthr = ws.thr[i0 + lane];
-                    tw = w ? w[i0 + lane] : 1.f;
-                }
-                uint32_t e_idx[PF];
-                float e_val[PF];
+        const int64_t cbase = c * CHUNK;
+        for (int64_t i0 = 0; i0 < n; i0 += PF) {
+            // lanes 0..PF-1 fetch the per-row state of rows i0..i0+PF-1
+            uint2 te = make_uint2(0, 0);
+            uint32_t tthr = 0, ttie = 0;
+            float tw = 1.f;
+            if (lane < PF && i0 + lane < n) {
+                te = ws.tab[c * n + i0 + lane];
+                tthr = ws.thr[i0 + lane];
+                ttie = (ws.flags[i0 + lane] & (F_TIES | F_EXACT)) == F_TIES;
+                tw = w ? w[i0 + lane] : 1.f;
+            }
+            uint32_t e_idx[PF];
+            float e_val[PF];
 #pragma unroll
-                for (int q = 0; q < PF; ++q) {
-                    const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
-                    e_idx[q] = 0;
-                    e_val[q] = 0.f;
-                    if ((uint32_t)lane < cnt && i0 + q < n) {
-                        e_idx[q] = ws.ent_idx[(i0 + q) * ws.cap + off + lane];
-                        e_val[q] = ws.ent_val[(i0 + q) * ws.cap + off + lane];
-                    }
+            for (int q = 0; q < PF; ++q) {
+                const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
+                e_idx[q] = 0;
+                e_val[q] = 0.f;
+                if ((uint32_t)lane < cnt && i0 + q < n) {
+                    e_idx[q] = ws.ent_idx[(i0 + q) * ws.cap + off + lane];
+                    e_val[q] = ws.ent_val[(i0 + q) * ws.cap + off + lane];
                 }
+            }
 #pragma unroll
-                for (int q = 0; q < PF; ++q) {
-                    if (i0 + q >= n) break;
-                    const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
-                    const uint32_t T = __shfl(tthr, q, WAVE);
-                    const float wi = __shfl(tw, q, WAVE);
-                    if ((uint32_t)lane < cnt && mag_key(e_val[q]) >= T) {
-                        const int loc = (int)(e_idx[q] - (uint32_t)cbase);
-                        if (ASSIGN) tl[loc] = e_val[q];
-                        else tl[loc] = tl[loc] + wi * e_val[q];
-                    }
-                    for (uint32_t e = 64 + lane; e < cnt; e += 64) {     // long lists (rare)
-                        const uint32_t ix = ws.ent_idx[(i0 + q) * ws.cap + off + e];
-                        const float vv = ws.ent_val[(i0 + q) * ws.cap + off + e];
-                        if (mag_key(vv) >= T) {
-                            const int loc = (int)(ix - (uint32_t)cbase);
-                            if (ASSIGN) tl[loc] = vv;
-                            else tl[loc] = tl[loc] + wi * vv;
-                        }
+            for (int q = 0; q < PF; ++q) {
+                if (i0 + q >= n) break;
+                const int64_t row = i0 + q;
+                const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
+                const uint32_t T = __shfl(tthr, q, WAVE);
+                const bool tiemode = __shfl(ttie, q, WAVE) != 0;
+                const float wi = __shfl(tw, q, WAVE);
+                for (uint32_t e0 = 0; e0 < cnt; e0 += 64) {
+                    const uint32_t e = e0 + lane;
+                    if (e >= cnt) continue;
+                    uint32_t ix;
+                    float vv;
+                    if (e0 == 0) { ix = e_idx[q]; vv = e_val[q]; }          // prefetched
+                    else { ix = ws.ent_idx[row * ws.cap + off + e]; vv = ws.ent_val[row * ws.cap + off + e]; }
+                    const uint32_t key = mag_key(vv);
+                    bool ok = key >= T;
+                    if (tiemode && key == T) ok = tie_admitted(ws, row, c, n, off, cnt, T, ix);
+                    if (ok) {
+                        const int loc = (int)(ix - (uint32_t)cbase);
+                        if (ASSIGN) tl[loc] = vv;
+                        else tl[loc] = tl[loc] + wi * vv;
                     }
                 }
             }
-            const int64_t len = min((int64_t)CHUNK, d - cbase);
-            for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
         }
+        const int64_t len = min((int64_t)CHUNK, d - cbase);
+        for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
     }
 }
 
@@ -607,10 +750,10 @@ hipLaunchKernelGGL(k_randk_scatter, g, dim3(256), 0, st, rows, n, d, K, p, ldi, 
             { ProfScope _ps("k_topk_sample", st);
 hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, K, ws); }
             FLC_CHECK_LAUNCH("k_topk_sample");
-            int gb = grid_stride_blocks(n * bpr, 8192);
             { ProfScope _ps("k_topk_filter", st);
-if (vec) hipLaunchKernelGGL((k_topk_filter<false, true>), dim3(gb), dim3(256), 0, st, rows, n, d, ws);
-            else hipLaunchKernelGGL((k_topk_filter<false, false>), dim3(gb), dim3(256), 0, st, rows, n, d, ws); }
+            const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((n * C + 3) / 4, 4096));
+            if (vec) hipLaunchKernelGGL((k_topk_filter_fast<true>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+            else hipLaunchKernelGGL((k_topk_filter_fast<false>), dim3(gw), dim3(256), 0, st, rows, n, d, ws); }
             FLC_CHECK_LAUNCH("k_topk_filter");
             const int64_t hb = (ws.cap + 65535) / 65536;
             for (int p = 0; p < 3; ++p) {
@@ -620,6 +763,11 @@ hipLaunchKernelGGL((k_radix_hist<false>), dim3(grid_stride_blocks(n * hb)), dim3
                 hipLaunchKernelGGL((k_radix_select<false>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, p, K, ws);
                 FLC_CHECK_LAUNCH("k_radix_select");
             }
+            // ambiguous ties at the K-th magnitude stay on the fast path: tie prefix per chunk
+            hipLaunchKernelGGL(k_cand_tie_count, dim3(grid_stride_blocks(n * bpr, 4096)), dim3(256), 0, st, n, d, ws);
+            FLC_CHECK_LAUNCH("k_cand_tie_count");
+            hipLaunchKernelGGL((k_tie_scan<false>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, d, ws);
+            FLC_CHECK_LAUNCH("k_tie_scan");
         } else {
             FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
         }
@@ -636,7 +784,7 @@ hipLaunchKernelGGL((k_radix_hist<true>), dim3(grid_stride_blocks(n * hb)), dim3(
         }
         hipLaunchKernelGGL(k_tie_count, dim3(grid_stride_blocks(n * bpr, 4096)), dim3(256), 0, st, rows, n, d, ws);
         FLC_CHECK_LAUNCH("k_tie_count");
-        hipLaunchKernelGGL(k_tie_scan, dim3(grid_stride_blocks(n, 1024)), dim3(64), 0, st, n, d, ws);
+        hipLaunchKernelGGL((k_tie_scan<true>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, d, ws);
         FLC_CHECK_LAUNCH("k_tie_scan");
         int gb = grid_stride_blocks(n * bpr, 8192);
         { ProfScope _ps("k_topk_filter_exact", st);

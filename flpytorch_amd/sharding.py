@@ -1,0 +1,70 @@
+"""Clients sharded across GPUs: one process per GPU, a [D] partial per GPU, one collective.
+
+The reference's only multi-GPU scheme is worker threads round-robin over a `--gpu` device list
+with a per-client `.to(device)` copy to the master inside every serverGradient
+(fl_pytorch/utils/thread_pool.py:59; algorithms.py:1756, 1763).  Here each rank owns a
+contiguous block of the round's clients, encodes + reduces them locally in client order
+(flc_encode_reduce with fp32 divisor 1.0, i.e. the exact partial sum) and the partials meet in a
+single collective over RCCL/xGMI (torch.distributed backend "nccl" on ROCm; "gloo" in the CPU
+tests).  Then every rank divides by the global weight.
+
+Two combine modes:
+  * "allreduce" — one all-reduce(SUM) of D floats (bandwidth-optimal; RCCL's sum order);
+  * "ordered"   — all-gather of the partials and a fixed rank-order fold: the result depends
+                  only on the client->rank blocks, bit-reproducible run to run.
+"""
+import torch
+import torch.distributed as dist
+
+
+def client_block(n_clients, world, rank):
+    """Contiguous, balanced block [lo, hi) of client positions owned by `rank`."""
+    base, extra = divmod(n_clients, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+class ShardedUplink:
+    """Round-level uplink over a process group.
+
+    encode_partial(rows, client0, out) must write sum_i w_i C_i(rows_i) (no division) into `out`
+    — the product passes an UplinkReducer with divisor=1.0; tests may pass an oracle callable.
+    """
+
+    def __init__(self, encode_partial, group=None, mode="allreduce"):
+        if mode not in ("allreduce", "ordered"):
+            raise ValueError(mode)
+        self.encode_partial = encode_partial
+        self.group = group
+        self.mode = mode
+
+    def __call__(self, rows, client0, total_weight, out=None):
+        world = dist.get_world_size(self.group)
+        d = rows.shape[1] if torch.is_tensor(rows) else rows[0].numel()
+        dev = rows.device if torch.is_tensor(rows) else rows[0].device
+        if out is None:
+            out = torch.empty(d, dtype=torch.float32, device=dev)
+        n_local = rows.shape[0] if torch.is_tensor(rows) else len(rows)
+        if n_local:
+            self.encode_partial(rows, client0, out)
+        else:
+            out.zero_()
+        if world > 1:
+            if self.mode == "allreduce":
+                dist.all_reduce(out, group=self.group)
+            else:
+                parts = [torch.empty_like(out) for _ in range(world)]
+                dist.all_gather(parts, out, group=self.group)
+                out.copy_(parts[0])
+                for p in parts[1:]:
+                    out.add_(p)
+        out.div_(float(total_weight))
+        return out
+
+
+def product_partial(reducer):
+    """encode_partial backed by the HIP kernels (flc_encode_reduce, fp32 divisor 1.0)."""
+
+    def run(rows, client0, out):
+        reducer(rows, out=out, client0=client0, divisor=1.0)
+    return run

@@ -147,9 +147,15 @@ int flc_mt_choice(uint32_t* h_key, int32_t* h_pos, int64_t n, int64_t k, int64_t
 int flc_mt_rand(uint32_t* h_key, int32_t* h_pos, int64_t n, double* h_out);
 int flc_mt_randint31(uint32_t* h_key, int32_t* h_pos, int64_t count, int64_t* h_out);
 
-/* Device-RNG mode, host mirror: the uniform / index the kernels draw for (seed, client, j). */
+/* Device-RNG mode, host mirror: the uniform (a multiple of 2^-32) / the RandK index set the
+ * kernels draw for (seed, client, element). */
 double flc_device_uniform(uint64_t seed, int64_t client, int64_t j);
 int flc_device_randk_indices(uint64_t seed, int64_t client, int64_t d, int64_t k, int64_t* h_out);
+
+/* Self-test of the exact fast fp32 division the dithering kernels use: for each of the n
+ * device divisors, every float numerator in [2^-80, 2^80] is divided both ways and the
+ * mismatches are written to d_mismatches[n] (device).  Must be all zero. */
+int flc_selftest_division(const float* d_divisors, int n, unsigned long long* d_mismatches, void* stream);
 
 /* ----------------------------------------------------------------------------------------
  * Kernel timing (off by default).  While enabled, every launch of the named hot kernels is

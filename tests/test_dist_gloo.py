@@ -1,0 +1,105 @@
+"""World-size-2 (and 3) gloo tests of the client sharding + combine path on CPU.
+
+The encoder here is the oracle (the HIP encoder is covered by tests/test_gpu_parity.py); what is
+tested is the distributed orchestration: client blocks, client ids per rank (device-RNG keys /
+compat stream positions), the partial-sum contract, both combine modes, and that the sharded
+result equals the single-process sequential result (bit-exact for 'ordered' when every rank
+holds one block; within fp32 reassociation otherwise).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from flpytorch_amd.sharding import ShardedUplink, client_block
+from oracle import codecs as oc
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def make_rows(n, d):
+    return np.random.default_rng(7).standard_normal((n, d)).astype(np.float32)
+
+
+def oracle_partial(spec, d):
+    def run(rows, client0, out):
+        enc = []
+        for i in range(rows.shape[0]):
+            o = oc.OracleCompressor(spec, d)
+            if o.type == oc.TOPK or o.type == oc.IDENTICAL:
+                enc.append(o.compress(rows[i].numpy()))
+            else:
+                raise ValueError("deterministic codecs only in this test")
+        acc = enc[0].copy()
+        for e in enc[1:]:
+            acc = acc + e
+        out.copy_(torch.from_numpy(acc))
+    return run
+
+
+def _worker(rank, world, port, spec, n, d, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = make_rows(n, d)
+    lo, hi = client_block(n, world, rank)
+    up = ShardedUplink(oracle_partial(spec, d), mode=mode)
+    out = up(torch.from_numpy(rows[lo:hi].copy()), client0=lo, total_weight=float(n))
+    q.put((rank, out.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode", ["allreduce", "ordered"])
+@pytest.mark.parametrize("spec", ["topk:5%", "ident"])
+def test_sharded_uplink_matches_single_process(world, mode, spec):
+    n, d = 7, 4099
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, spec, n, d, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rows = make_rows(n, d)
+    enc = [oc.OracleCompressor(spec, d).compress(rows[i]) for i in range(n)]
+    want = oc.reduce_plain(enc)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r], res[0])            # every rank holds the same result
+        np.testing.assert_allclose(res[r], want, rtol=2e-6, atol=1e-7)
+    if mode == "ordered":
+        # fixed fold: (block0 + block1 + ...) / n, reproducible
+        parts = []
+        for r in range(world):
+            lo, hi = client_block(n, world, r)
+            acc = enc[lo].copy()
+            for e in enc[lo + 1:hi]:
+                acc = acc + e
+            parts.append(acc)
+        fold = parts[0].copy()
+        for p in parts[1:]:
+            fold = fold + p
+        np.testing.assert_array_equal(res[0], fold / np.float32(n))
+
+
+@pytest.mark.parametrize("n,world", [(7, 2), (8, 8), (3, 4), (4096, 8), (1, 1)])
+def test_client_blocks_partition(n, world):
+    seen = []
+    for r in range(world):
+        lo, hi = client_block(n, world, r)
+        assert 0 <= lo <= hi <= n
+        seen.extend(range(lo, hi))
+    assert seen == list(range(n))

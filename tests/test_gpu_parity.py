@@ -299,3 +299,21 @@ def test_randk_scale_inexact(ag):
     S = c.S.cpu().numpy()
     want[S] = np.float32(d / c.K) * x[S]
     assert_bitexact(out, want)
+
+
+def test_fast_division_selftest(ag):
+    """The dithering kernels' Markstein division == IEEE division for every float numerator in
+    [2^-80, 2^80], for norms / level gaps of every kind (random, powers of two, all-ones mantissa,
+    the qsgd:127 level gap)."""
+    from flpytorch_amd import _lib
+    lib = _lib.load()
+    g = np.random.default_rng(11)
+    bs = list(np.float32(g.uniform(1, 2, 24)) * np.float32(2.0) ** g.integers(-30, 60, 24).astype(np.float32))
+    bs += [np.float32(1.0), np.float32(3.0), np.float32(0.1), np.uint32(0x3FFFFFFF).view(np.float32),
+           np.uint32(0x4B7FFFFF).view(np.float32), -np.float32(1.0 / 127), np.float32(0.0078740157),
+           -np.float32(np.float32(2.0 / 127) - np.float32(1.0 / 127))]
+    b = torch.tensor(np.array(bs, dtype=np.float32), device="cuda")
+    bad = torch.zeros(len(bs), dtype=torch.int64, device="cuda")
+    _lib.check(lib.flc_selftest_division(b.data_ptr(), len(bs), bad.data_ptr(), _lib.stream_ptr()), "selftest")
+    torch.cuda.synchronize()
+    assert bad.cpu().tolist() == [0] * len(bs)
