@@ -13,6 +13,7 @@ Workloads (BASELINE.json configs; the default is the largest single-GPU config, 
   c3  topk:1%   N=1024 / GPU, D=10 M   (ResNet-18-sized)                     [default]
   c2  randk:1%  N=256  / GPU, D=1 M    (device-RNG indices)
   c4  qsgd:127  N=512  / GPU, D=25 M   (C4's per-GPU shard: at --gpus 8 this IS C4, N=4096)
+  reduce  ident N=512 / GPU, D=25 M   (the serverGradient fold alone)
 
 Algorithmic bytes: topk / qsgd / ident 4*N*D + 4*D; randk 4*N*K + 4*D (device-RNG
 indices cost no bytes).  value = algorithmic bytes of all ranks / max-over-ranks step time.
@@ -42,6 +43,8 @@ WORKLOADS = {
     "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2),
     "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_scatter", config=1),
     "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ew_accum_vec", config=3),
+    # the serverGradient fold alone (identity codec), C4's shard shape
+    "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3),
 }
 
 
@@ -55,7 +58,7 @@ def kernel_bytes(kernel, n, d, k):
     """Algorithmic bytes one launch of the dominant kernel must move."""
     if kernel == "k_randk_scatter":
         return 8 * n * k            # gather K values per row + write K (idx, value) entries
-    if kernel == "k_ew_accum_vec":
+    if kernel in ("k_ew_accum_vec", "k_reduce_vec"):
         return 4 * n * d + 4 * d    # read every row once, write the [D] result
     return 4 * n * d                # k_topk_filter: read every row once
 
@@ -87,6 +90,65 @@ def cpu_baseline(spec, d, budget_s=12.0):
                       f"({dt:.1f} s, numpy single-threaded)"}
 
 
+def e2e(args):
+    """Host-resident uplink: rows in pinned host memory -> H2D -> flc_encode_reduce -> D2H, one GPU.
+    The rows are streamed in blocks of `blk` clients on two streams so the H2D copy of block k+1
+    overlaps the encode of block k; partial sums (divisor 1.0) are folded on device."""
+    from flpytorch_amd import aggregation as ag
+    wl = dict(WORKLOADS[args.workload])
+    n = args.n or 64
+    d = args.d or wl["d"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comp = ag.initCompressor(wl["spec"], d)
+    k = getattr(comp, "K", 0) or 0
+    g = torch.Generator(device=dev).manual_seed(5)
+    blk = 8
+    host = torch.empty((n, d), dtype=torch.float32, pin_memory=True)
+    for i in range(0, n, blk):
+        host[i:i + blk].copy_(torch.randn((min(blk, n - i), d), generator=g, device=dev))
+    bufs = [torch.empty((blk, d), dtype=torch.float32, device=dev) for _ in range(2)]
+    part = torch.empty(d, dtype=torch.float32, device=dev)
+    acc = torch.empty(d, dtype=torch.float32, device=dev)
+    out_host = torch.empty(d, dtype=torch.float32, pin_memory=True)
+    red = ag.UplinkReducer(comp, device=dev, seed=7)
+    copy_s, comp_s = torch.cuda.Stream(), torch.cuda.current_stream()
+
+    def step():
+        evs = []
+        for b, i in enumerate(range(0, n, blk)):
+            buf = bufs[b % 2]
+            m = min(blk, n - i)
+            with torch.cuda.stream(copy_s):
+                if b >= 2:
+                    copy_s.wait_event(evs[b - 2])        # buffer free again
+                buf[:m].copy_(host[i:i + m], non_blocking=True)
+                ready = torch.cuda.Event()
+                ready.record(copy_s)
+            comp_s.wait_event(ready)
+            red(buf[:m], out=part if i else acc, client0=i, divisor=1.0)
+            if i:
+                acc.add_(part)
+            done = torch.cuda.Event()
+            done.record(comp_s)
+            evs.append(done)
+        acc.div_(float(n))
+        out_host.copy_(acc, non_blocking=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    moved = 4 * n * d + 4 * d
+    print(json.dumps({"mode": "end-to-end host->device->host", "codec": wl["spec"], "clients": n, "D": d, "K": k,
+                      "ms_per_step": round(dt * 1e3, 3), "pcie_inclusive_GBps": round(moved / dt / 1e9, 2),
+                      "note": "rows start in pinned host memory; 2-stream H2D/encode overlap, blocks of 8 clients"}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,7 +158,12 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="end-to-end: client rows start in pinned host memory, the [D] result lands in host memory "
+                         "(H2D + encode+reduce + D2H per step; PCIe-bound; reported in DESIGN.md, never as value)")
     args = ap.parse_args()
+    if args.e2e:
+        return e2e(args)
 
     wl = dict(WORKLOADS[args.workload])
     if args.n:

@@ -341,18 +341,51 @@ struct DitherOp {
         const float lev = down ? t.x : t.y;
         return (x == 0.f) ? 0.f : copysignf(lev, x) * dn.b;
     }
+    // NE elements, written stage by stage (each step for all elements before the next) so the NE
+    // dependency chains are interleaved in the instruction stream; one fix-up branch at the end.
+    template <bool F, int NE>
+    __device__ inline void apply_block(const float* x, const int64_t* jv, const uint32_t* cs, const float4* tab,
+                                       float* out) const {
+        float y[NE], p2[NE];
+        float4 t[NE];
+        bool fix[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) y[e] = F ? div_fast(fabsf(x[e]), dn) : div_rn(fabsf(x[e]), dn);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            int g = (int)(y[e] * sf);
+            g = g > s - 1 ? s - 1 : g;
+            t[e] = tab[g];
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            fix[e] = (y[e] < t[e].x) | !(y[e] <= t[e].y);
+            FastDiv dd;
+            dd.b = t[e].z; dd.rb = t[e].w; dd.ok = true;
+            const float num = y[e] - t[e].y;
+            p2[e] = (F || t[e].w != 0.f) ? div_fast(num, dd) : num / t[e].z;
+        }
+        bool any = false;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const bool down = draw_below<COMPAT>(urow, rk, jv[e], cs[e], COMPAT ? ldexpf(p2[e], -32) : 0.f, p2[e]);
+            const float lev = down ? t[e].x : t[e].y;
+            out[e] = (x[e] == 0.f) ? 0.f : copysignf(lev, x[e]) * dn.b;
+            any |= fix[e];
+        }
+        if (any) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e)
+                if (fix[e]) out[e] = apply<F>(x[e], jv[e], cs[e], tab);
+        }
+    }
     template <bool F>
     __device__ inline float4 apply4(float4 v, int64_t j, const uint32_t* cs, const float4* tab) const {
-        bool f0, f1, f2, f3;
-        float4 r = make_float4(guess_elem<F>(v.x, j, cs[0], tab, f0), guess_elem<F>(v.y, j + 1, cs[1], tab, f1),
-                               guess_elem<F>(v.z, j + 2, cs[2], tab, f2), guess_elem<F>(v.w, j + 3, cs[3], tab, f3));
-        if (f0 | f1 | f2 | f3) {
-            if (f0) r.x = apply<F>(v.x, j, cs[0], tab);
-            if (f1) r.y = apply<F>(v.y, j + 1, cs[1], tab);
-            if (f2) r.z = apply<F>(v.z, j + 2, cs[2], tab);
-            if (f3) r.w = apply<F>(v.w, j + 3, cs[3], tab);
-        }
-        return r;
+        const float x[4] = {v.x, v.y, v.z, v.w};
+        const int64_t jv[4] = {j, j + 1, j + 2, j + 3};
+        float o[4];
+        apply_block<F, 4>(x, jv, cs, tab, o);
+        return make_float4(o[0], o[1], o[2], o[3]);
     }
 };
 
@@ -363,6 +396,29 @@ __device__ inline float4 apply4(const Op& op, float4 v, int64_t j, const uint32_
     } else {
         return make_float4(op.template apply<F>(v.x, j, cs[0], tab), op.template apply<F>(v.y, j + 1, cs[1], tab),
                            op.template apply<F>(v.z, j + 2, cs[2], tab), op.template apply<F>(v.w, j + 3, cs[3], tab));
+    }
+}
+
+// COLS float4 groups of one row at once (dithering: one interleaved block, one fix-up branch)
+template <bool F, int COLS, class Op>
+__device__ inline void apply_cols(const Op& op, const float4* v, const int64_t* gi, const uint32_t (*cs)[4],
+                                  const float4* tab, float4* e) {
+    if constexpr (Op::HAS_APPLY4) {
+        float x[COLS * 4], o[COLS * 4];
+        int64_t jv[COLS * 4];
+        uint32_t c2[COLS * 4];
+#pragma unroll
+        for (int c = 0; c < COLS; ++c) {
+            x[4 * c] = v[c].x; x[4 * c + 1] = v[c].y; x[4 * c + 2] = v[c].z; x[4 * c + 3] = v[c].w;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { jv[4 * c + q] = gi[c] * 4 + q; c2[4 * c + q] = cs[c][q]; }
+        }
+        op.template apply_block<F, COLS * 4>(x, jv, c2, tab, o);
+#pragma unroll
+        for (int c = 0; c < COLS; ++c) e[c] = make_float4(o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
+    } else {
+#pragma unroll
+        for (int c = 0; c < COLS; ++c) e[c] = apply4<F>(op, v[c], gi[c] * 4, cs[c], tab);
     }
 }
 
@@ -449,13 +505,10 @@ __global__ __launch_bounds__(256) void k_ew_accum_vec(RowSrc src, int64_t n, int
                     op.setup(i);
                     const float wi = W ? w[i] : 1.f;
                     float4 e[COLS];
-                    if (op.row_fast()) {   // row-uniform: whole row inside the fast-division window
-#pragma unroll
-                        for (int c = 0; c < COLS; ++c) e[c] = apply4<true>(op, ring[p][c], gi[c] * 4, cs[c], smem_tab);
-                    } else {
-#pragma unroll
-                        for (int c = 0; c < COLS; ++c) e[c] = apply4<false>(op, ring[p][c], gi[c] * 4, cs[c], smem_tab);
-                    }
+                    if (op.row_fast())     // row-uniform: whole row inside the fast-division window
+                        apply_cols<true, COLS>(op, ring[p], gi, cs, smem_tab, e);
+                    else
+                        apply_cols<false, COLS>(op, ring[p], gi, cs, smem_tab, e);
 #pragma unroll
                     for (int c = 0; c < COLS; ++c) {
                         const float4 t = W ? make_float4(wi * e[c].x, wi * e[c].y, wi * e[c].z, wi * e[c].w) : e[c];

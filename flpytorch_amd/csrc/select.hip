@@ -312,20 +312,33 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t C = nchunks(d);
     const int64_t items = n * C;
+    const int64_t stride = (int64_t)gridDim.x * 4;
     uint32_t* si = st_idx[wv];
     float* sv = st_val[wv];
-    for (int64_t it = (int64_t)blockIdx.x * 4 + wv; it < items; it += (int64_t)gridDim.x * 4) {
+    int64_t it = (int64_t)blockIdx.x * 4 + wv;
+    if (it >= items) return;
+    // software pipeline across chunks: the next chunk's first stage is in flight while this
+    // chunk's last stage is compacted and its entries are reserved (atomic) and copied out
+    float4 cur[4], nxt[4];
+    {
+        const int64_t row = it / C;
+        load_stage<VEC>(rows.row(row), (it - row * C) * CHUNK, 0, lane, d, cur);
+    }
+    while (it < items) {
         const int64_t row = it / C, c = it - row * C;
-        if (ws.flags[row]) continue;                       // row already failed (wave-uniform)
         const float* r = rows.row(row);
         const uint32_t T = ws.thr[row];
         const int64_t j0 = c * CHUNK;
+        const int64_t nit = it + stride;
         uint32_t cnt = 0;
-        float4 cur[4], nxt[4];
-        load_stage<VEC>(r, j0, 0, lane, d, cur);
 #pragma unroll
         for (int sg = 0; sg < 4; ++sg) {
-            if (sg < 3) load_stage<VEC>(r, j0, sg + 1, lane, d, nxt);
+            if (sg < 3) {
+                load_stage<VEC>(r, j0, sg + 1, lane, d, nxt);
+            } else if (nit < items) {
+                const int64_t nrow = nit / C;
+                load_stage<VEC>(rows.row(nrow), (nit - nrow * C) * CHUNK, 0, lane, d, nxt);
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int64_t j = j0 + (int64_t)((sg * 4 + u) * 64 + lane) * 4;
@@ -343,10 +356,8 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
                     }
                 }
             }
-            if (sg < 3) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-            }
+            for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
         }
         bool fits = cnt <= STCAP;
         uint32_t base = 0;
@@ -366,6 +377,7 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
             for (uint32_t e = lane; e < cnt; e += 64) { oi[e] = si[e]; ov[e] = sv[e]; }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // reads done before the next chunk's writes
+        it = nit;
     }
 }
 

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""HBM traffic of the bench's dominant kernel from rocprofv3 PMC counters (run on the GPU box).
+
+Two separate passes (FETCH_SIZE and WRITE_SIZE cannot share one: MI355X_MICROARCH.md "rocprofv3
+PMC slots"), each `rocprofv3 --pmc <ctr> -- python bench.py --workload <wl> ...`, then:
+
+    hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 / launches
+
+FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts exactly half the bytes of a wide
+(16 B/lane) coalesced streaming read, hence the factor 2 (MI355X_MICROARCH.md §HBM,
+cdna_hip_programming.md §7).  Writes to profiles/pmc_<wl>.json, which bench.py reads into
+roofline.traffic.
+
+usage: python tools/collect_pmc.py --workload c3 [--n N] [--steps 2]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL_SUBSTR = {"c3": "k_topk_filter_fast", "c4": "k_ew_accum_vec", "reduce": "k_reduce_vec",
+                 "c2": "k_randk_scatter"}
+
+
+def run_pass(ctr, wl, extra, outdir):
+    cmd = ["rocprofv3", "--pmc", ctr, "-d", outdir, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--no-cpu-baseline"] + extra
+    subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL, timeout=600)
+    vals, disp = collections.defaultdict(float), set()
+    for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if KERNEL_SUBSTR[wl] in r["Kernel_Name"]:
+                vals[r["Counter_Name"]] += float(r["Counter_Value"])
+                disp.add(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+    return vals[ctr], len(disp)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=2)
+    a = ap.parse_args()
+    extra = ["--steps", str(a.steps), "--warmup", "1"] + (["--n", str(a.n)] if a.n else [])
+    os.environ.setdefault("TMPDIR", "/tmp")
+    base = os.path.join(ROOT, "gpurun_out", f"pmc_traffic_{a.workload}")
+    fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch")
+    write, nw = run_pass("WRITE_SIZE", a.workload, extra, base + "_write")
+    launches = max(nf, nw, 1)
+    res = {"workload": a.workload, "kernel": KERNEL_SUBSTR[a.workload], "n_override": a.n,
+           "launches": launches, "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
+           "hbm_bytes_per_launch": int((2 * fetch + write) * 1024 / launches),
+           "correction": "2 x FETCH_SIZE (gfx950 counts half of 16 B/lane streaming reads) + WRITE_SIZE, KiB->B"}
+    for d in ("profiles", "gpurun_out"):       # gpurun_out/ is what travels back from the GPU box
+        os.makedirs(os.path.join(ROOT, d), exist_ok=True)
+        with open(os.path.join(ROOT, d, f"pmc_{a.workload}.json"), "w") as f:
+            json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
