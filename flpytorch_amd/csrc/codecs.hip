@@ -615,11 +615,11 @@ static int launch_accum(RowSrc src, bool vec, int64_t n, int64_t d, Op op, const
     if (vec && ((uintptr_t)out & 15u) == 0) {
         if (d / 4 > 0) {
             switch (ew_tile_variant()) {
-                case 1: launch_accum_tile<Op, 2, 2>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+                case 2: launch_accum_tile<Op, 2, 4>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
                 case 3: launch_accum_tile<Op, 1, 8>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
                 case 4: launch_accum_tile<Op, 1, 4>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
                 case 5: launch_accum_tile<Op, 4, 2>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
-                default: launch_accum_tile<Op, 2, 4>(src, n, d, op, levels, s, w, wt, out, lds, st); break;
+                default: launch_accum_tile<Op, 2, 2>(src, n, d, op, levels, s, w, wt, out, lds, st); break;  // measured best (C4)
             }
             FLC_CHECK_LAUNCH("k_ew_accum_vec");
         }

@@ -58,11 +58,23 @@ struct Carver {
 
 // Row addressing shared by every kernel: a strided matrix (row i at base + i*ld) or a device
 // array of row pointers (base == nullptr).
+// Scalar (constant address space) load of a wave-uniform address: the data must not change
+// during the kernel (written by earlier launches only).
+template <class T>
+__device__ inline T sload(const T* p) {
+    return *(const __attribute__((address_space(4))) T*)p;
+}
+
 struct RowSrc {
     const float* base;
     int64_t ld;
     const float* const* ptrs;
     __device__ inline const float* row(int64_t i) const { return base ? base + i * ld : ptrs[i]; }
+    // wave-uniform i: the pointer table is read through the scalar cache (s_load, lgkmcnt), so it
+    // does not join the vector-memory queue of a streaming pipeline
+    __device__ inline const float* row_s(int64_t i) const {
+        return base ? base + i * ld : sload(ptrs + i);
+    }
 };
 
 // Internal entry points of the codec families (reduce.hip, codecs.hip, select.hip).

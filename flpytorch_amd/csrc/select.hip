@@ -45,7 +45,7 @@ struct SelWs {            // carved from the caller workspace
     int64_t cap;
 };
 
-__device__ inline int64_t nchunks(int64_t d) { return (d + CHUNK - 1) >> CHUNK_SHIFT; }
+__host__ __device__ inline int64_t nchunks(int64_t d) { return (d + CHUNK - 1) >> CHUNK_SHIFT; }
 
 // ------------------------------------------------------------------------------------------
 // Block-level helpers
@@ -286,99 +286,126 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
 // one atomic reserves the row-buffer space and the staging is copied out coalesced.  Register
 // footprint stays small so 8 waves per SIMD keep the HBM pipe full.
 // ------------------------------------------------------------------------------------------
-constexpr int STCAP = 512;           // staged entries per chunk (12.5 %; more -> row overflow)
+constexpr int STCAP = 320;           // staged entries per chunk (7.8 %, ~6x the 1 % mean; more -> row overflow)
+static_assert(STCAP % 64 == 0, "copy-out runs in whole wave slots");
 
-template <bool VEC>
-__device__ inline void load_stage(const float* r, int64_t j0, int sg, int lane, int64_t d, float4 (&v)[4]) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + (int64_t)((sg * 4 + u) * 64 + lane) * 4;
-        if (VEC && j + 3 < d) {
-            v[u] = *reinterpret_cast<const float4*>(r + j);
-        } else {
-            v[u].x = (j < d) ? r[j] : 0.f;
-            v[u].y = (j + 1 < d) ? r[j + 1] : 0.f;
-            v[u].z = (j + 2 < d) ? r[j + 2] : 0.f;
-            v[u].w = (j + 3 < d) ? r[j + 3] : 0.f;
-        }
-    }
+// One stage = 4 x 1 KB of a chunk per wave, through a buffer descriptor built from the wave-uniform
+// chunk base (SGPRs): 32-bit lane offsets, no 64-bit address VGPRs, and the hardware range check
+// returns 0 past the row's end (the tail needs no scalar path).
+__device__ inline __amdgpu_buffer_rsrc_t chunk_rsrc(const float* r, int64_t j0, int64_t d) {
+    const int64_t len = min((int64_t)CHUNK, d - j0);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r + j0), (short)0, (int)(len * 4), 0x00020000);
+}
+__device__ inline float4 load_q(__amdgpu_buffer_rsrc_t rs, int lane, int L) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, L * 1024, 0);
+    return make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
 }
 
-template <bool VEC>
+// A chunk is 16 wave-loads of 1 KB.  RING float4 registers per lane hold a software pipeline RING-1
+// loads deep that runs across chunk boundaries (the next item's descriptor is built up front; past
+// the last item it has num_records 0 and its loads return zeros without touching memory).
+template <int RING>
 __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
-    __shared__ uint32_t st_idx[4][STCAP];
-    __shared__ float st_val[4][STCAP];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
+    // two staging buffers per wave: chunk i compacts into one while chunk i-1's reservation (the
+    // atomic issued at the end of i-1) is consumed and its entries are copied out of the other;
+    // the atomic's return never stalls the load pipeline
+    __shared__ uint32_t st_idx[2][4][STCAP];
+    __shared__ float st_val[2][4][STCAP];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t C = nchunks(d);
     const int64_t items = n * C;
     const int64_t stride = (int64_t)gridDim.x * 4;
-    uint32_t* si = st_idx[wv];
-    float* sv = st_val[wv];
     int64_t it = (int64_t)blockIdx.x * 4 + wv;
     if (it >= items) return;
-    // software pipeline across chunks: the next chunk's first stage is in flight while this
-    // chunk's last stage is compacted and its entries are reserved (atomic) and copied out
-    float4 cur[4], nxt[4];
-    {
-        const int64_t row = it / C;
-        load_stage<VEC>(rows.row(row), (it - row * C) * CHUNK, 0, lane, d, cur);
+    float4 ring[RING];
+    int64_t row = it / C;
+    auto rs = chunk_rsrc(rows.row_s(row), (it - row * C) * CHUNK, d);
+#pragma unroll
+    for (int L = 0; L < RING - 1; ++L) {
+        ring[L] = load_q(rs, lane, L);
+        __builtin_amdgcn_sched_barrier(0);   // issue in ring order: the loop's static vmcnt waits assume it
     }
-    while (it < items) {
-        const int64_t row = it / C, c = it - row * C;
-        const float* r = rows.row(row);
-        const uint32_t T = ws.thr[row];
-        const int64_t j0 = c * CHUNK;
-        const int64_t nit = it + stride;
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int sg = 0; sg < 4; ++sg) {
-            if (sg < 3) {
-                load_stage<VEC>(r, j0, sg + 1, lane, d, nxt);
-            } else if (nit < items) {
-                const int64_t nrow = nit / C;
-                load_stage<VEC>(rows.row(nrow), (nit - nrow * C) * CHUNK, 0, lane, d, nxt);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t j = j0 + (int64_t)((sg * 4 + u) * 64 + lane) * 4;
-                const float vq[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
-                const int any = (int)(mag_key(vq[0]) >= T) | (int)(mag_key(vq[1]) >= T) |
-                                (int)(mag_key(vq[2]) >= T) | (int)(mag_key(vq[3]) >= T);
-                if (__ballot(any)) {                      // ~1-2 % of elements: most groups skip
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const bool f = (j + q < d) && mag_key(vq[q]) >= T;
-                        const uint64_t m = __ballot(f);
-                        const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
-                        if (f && pos < STCAP) { si[pos] = (uint32_t)(j + q); sv[pos] = vq[q]; }
-                        cnt += (uint32_t)__popcll(m);
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-        }
-        bool fits = cnt <= STCAP;
+    // previous chunk, reservation in flight
+    bool pv = false;
+    int64_t prow = 0, pc = 0;
+    uint32_t pcnt = 0, pres = 0;
+    int par = 0;
+    auto finish = [&](int pb) {
         uint32_t base = 0;
-        if (fits && cnt) {
-            if (lane == 0) base = atomicAdd(&ws.rowcnt[row], cnt);
-            base = __shfl(base, 0, WAVE);
-            fits = (int64_t)base + cnt <= ws.cap;
+        bool fits = pcnt <= STCAP;
+        if (fits && pcnt) {
+            base = __shfl(pres, 0, WAVE);
+            fits = (int64_t)base + pcnt <= ws.cap;
         }
         if (lane == 0) {
-            ws.tab[c * n + row] = make_uint2(base, fits ? cnt : 0u);
-            if (!fits) atomicOr(&ws.flags[row], F_OVERFLOW);
+            ws.tab[pc * n + prow] = make_uint2(base, fits ? pcnt : 0u);
+            if (!fits) atomicOr(&ws.flags[prow], F_OVERFLOW);
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // staging writes -> reads (same wave)
         if (fits) {
-            uint32_t* oi = ws.ent_idx + row * ws.cap + base;
-            float* ov = ws.ent_val + row * ws.cap + base;
-            for (uint32_t e = lane; e < cnt; e += 64) { oi[e] = si[e]; ov[e] = sv[e]; }
+            const uint32_t* si = st_idx[pb][wv];
+            const float* sv = st_val[pb][wv];
+            uint32_t* oi = ws.ent_idx + prow * ws.cap + base;
+            float* ov = ws.ent_val + prow * ws.cap + base;
+            // fixed trip count (STCAP / 64 predicated slots): the compiler's vmcnt bookkeeping
+            // stays exact for the loads in flight behind these stores
+#pragma unroll
+            for (int k = 0; k < STCAP / 64; ++k) {
+                const uint32_t e = (uint32_t)(k * 64 + lane);
+                if (e < pcnt) { oi[e] = si[e]; ov[e] = sv[e]; }
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // reads done before the next chunk's writes
+    };
+    while (it < items) {
+        const int64_t c = it - row * C;
+        const int64_t j0 = c * CHUNK;
+        const uint32_t T = sload(ws.thr + row);
+        const uint32_t lim = (uint32_t)min((int64_t)CHUNK, d - j0);     // valid elements in this chunk
+        const int64_t nit = it + stride;
+        const int64_t nrow = nit < items ? nit / C : row;
+        const auto rsn = nit < items ? chunk_rsrc(rows.row_s(nrow), (nit - nrow * C) * CHUNK, d)
+                                     : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
+        uint32_t* si = st_idx[par][wv];
+        float* sv = st_val[par][wv];
+        uint32_t cnt = 0;
+        // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
+        // component) index constants out of the item loop into 64 live VGPRs
+        uint32_t lb = (uint32_t)lane * 4u;
+        asm volatile("" : "+v"(lb));
+#pragma unroll
+        for (int L = 0; L < 16; ++L) {
+            const int P = L + RING - 1;
+            ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
+            const float4 x = ring[L % RING];
+            const uint32_t jl = lb + (uint32_t)(L * 256);                 // offset inside the chunk
+            const float vq[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool f = (jl + q < lim) && mag_key(vq[q]) >= T;
+                const uint64_t m = __ballot(f);
+                if (m) {
+                    const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                    if (f && pos < STCAP) { si[pos] = (uint32_t)j0 + jl + q; sv[pos] = vq[q]; }
+                    cnt += (uint32_t)__popcll(m);
+                }
+            }
+        }
+        if (pv) finish(par ^ 1);
+        uint32_t res = 0;
+        if (cnt && cnt <= STCAP && lane == 0) res = atomicAdd(&ws.rowcnt[row], cnt);
+        pv = true; prow = row; pc = c; pcnt = cnt; pres = res;
+        // this chunk's staging writes before next-next chunk's reuse of the buffer are ordered by
+        // the wave's own program order; the fence keeps the compiler from moving LDS ops across
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        par ^= 1;
         it = nit;
+        row = nrow;
+        rs = rsn;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    finish(par ^ 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -729,6 +756,29 @@ static int grid_stride_blocks(int64_t items, int64_t cap = 4096) {
 }
 
 // Runs the TopK / RandK pipeline for n rows and writes out (ASSIGN: n == 1 dense encode).
+static int filter_ring() {
+    static const int r = [] {
+        const char* e = getenv("FLC_FILTER_RING");
+        return (e && atoi(e) == 16) ? 16 : 8;
+    }();
+    return r;
+}
+
+template <int RING>
+static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream_t st) {
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_topk_filter_fast<RING>, 256, 0);
+        resident = std::max(1, cus * std::max(1, per));
+    }
+    const int64_t waves = n * nchunks(d);
+    const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, resident));
+    hipLaunchKernelGGL((k_topk_filter_fast<RING>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+}
+
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
     const int codec = prm->codec;
@@ -763,9 +813,10 @@ hipLaunchKernelGGL(k_randk_scatter, g, dim3(256), 0, st, rows, n, d, K, p, ldi, 
 hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, K, ws); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             { ProfScope _ps("k_topk_filter", st);
-            const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((n * C + 3) / 4, 4096));
-            if (vec) hipLaunchKernelGGL((k_topk_filter_fast<true>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
-            else hipLaunchKernelGGL((k_topk_filter_fast<false>), dim3(gw), dim3(256), 0, st, rows, n, d, ws); }
+            // persistent grid: exactly the resident blocks (a second partial wave of blocks would
+            // leave the chip half idle at the end); buffer loads need no 16 B row alignment
+            if (filter_ring() == 8) launch_filter<8>(rows, n, d, ws, st);
+            else launch_filter<16>(rows, n, d, ws, st); }
             FLC_CHECK_LAUNCH("k_topk_filter");
             const int64_t hb = (ws.cap + 65535) / 65536;
             for (int p = 0; p < 3; ++p) {
