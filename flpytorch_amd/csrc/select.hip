@@ -280,20 +280,25 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
 }
 
 // ------------------------------------------------------------------------------------------
-// Fast-path filter: one wave per 4096-element chunk, grid-stride over (row, chunk).  The chunk
-// streams in 4 stages of 1 KB per lane-group with the next stage's loads in flight; entries
-// with key >= T_lo are compacted (ballot / mbcnt) into a wave-private LDS staging buffer, then
-// one atomic reserves the row-buffer space and the staging is copied out coalesced.  Register
-// footprint stays small so 8 waves per SIMD keep the HBM pipe full.
+// Fast-path filter.  A work item is a group of GS consecutive 4096-element chunks of one row; waves
+// walk items grid-stride.  Every chunk streams in through a RING-deep buffer-load pipeline that
+// runs across chunk and item boundaries; entries with key >= T_lo are compacted (ballot / mbcnt)
+// into a wave-private LDS staging buffer.  One atomic per group reserves the row-buffer space; its
+// return is consumed only after the NEXT group has been compacted (double-buffered staging), when
+// the group's entries are copied out coalesced and its GS tab entries are written.
+//
+// Why groups: on gfx950 vmcnt retires in order, so every atomic / store sits in front of the loads
+// issued after it.  Per-chunk reservations (one atomic + a short copy-out per 4096 elements) cost
+// ~20 % of the filter's bandwidth (tools/probe_filter.hip); a group of 4 amortises them 4x and the
+// copy-out stores become full 256 B wave writes.
 // ------------------------------------------------------------------------------------------
-constexpr int STCAP = 320;           // staged entries per chunk (7.8 %, ~6x the 1 % mean; more -> row overflow)
-static_assert(STCAP % 64 == 0, "copy-out runs in whole wave slots");
+constexpr int GCAP = 512;             // staged entries per group (4 chunks: 3.1 %, ~2.5x the mean at 1.2 %; more -> row overflow)
+static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 
-// One stage = 4 x 1 KB of a chunk per wave, through a buffer descriptor built from the wave-uniform
-// chunk base (SGPRs): 32-bit lane offsets, no 64-bit address VGPRs, and the hardware range check
-// returns 0 past the row's end (the tail needs no scalar path).
+// Buffer descriptor of one chunk built from the wave-uniform chunk base (SGPRs): 32-bit lane
+// offsets, no 64-bit address VGPRs, and the hardware range check returns 0 past the row's end.
 __device__ inline __amdgpu_buffer_rsrc_t chunk_rsrc(const float* r, int64_t j0, int64_t d) {
-    const int64_t len = min((int64_t)CHUNK, d - j0);
+    const int64_t len = max((int64_t)0, min((int64_t)CHUNK, d - j0));
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r + j0), (short)0, (int)(len * 4), 0x00020000);
 }
 __device__ inline float4 load_q(__amdgpu_buffer_rsrc_t rs, int lane, int L) {
@@ -302,107 +307,134 @@ __device__ inline float4 load_q(__amdgpu_buffer_rsrc_t rs, int lane, int L) {
 }
 
 // A chunk is 16 wave-loads of 1 KB.  RING float4 registers per lane hold a software pipeline RING-1
-// loads deep that runs across chunk boundaries (the next item's descriptor is built up front; past
-// the last item it has num_records 0 and its loads return zeros without touching memory).
-template <int RING>
+// loads deep (the next chunk's descriptor is built up front; past the last item it has
+// num_records 0 and its loads return zeros without touching memory).
+// FGS: chunks per work item (group).
+template <int RING, int FGS>
 __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
-    // two staging buffers per wave: chunk i compacts into one while chunk i-1's reservation (the
-    // atomic issued at the end of i-1) is consumed and its entries are copied out of the other;
-    // the atomic's return never stalls the load pipeline
-    __shared__ uint32_t st_idx[2][4][STCAP];
-    __shared__ float st_val[2][4][STCAP];
+    __shared__ uint32_t st_idx[2][4][GCAP];
+    __shared__ float st_val[2][4][GCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t C = nchunks(d);
-    const int64_t items = n * C;
+    const int64_t G = (C + FGS - 1) / FGS;                               // groups per row
+    const int64_t items = n * G;
     const int64_t stride = (int64_t)gridDim.x * 4;
     int64_t it = (int64_t)blockIdx.x * 4 + wv;
     if (it >= items) return;
     float4 ring[RING];
-    int64_t row = it / C;
-    auto rs = chunk_rsrc(rows.row_s(row), (it - row * C) * CHUNK, d);
+    int64_t row = it / G;
+    int64_t c = (it - row * G) * FGS;                                    // current chunk
+    auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
 #pragma unroll
     for (int L = 0; L < RING - 1; ++L) {
         ring[L] = load_q(rs, lane, L);
         __builtin_amdgcn_sched_barrier(0);   // issue in ring order: the loop's static vmcnt waits assume it
     }
-    // previous chunk, reservation in flight
+    // previous group, reservation in flight
     bool pv = false;
-    int64_t prow = 0, pc = 0;
-    uint32_t pcnt = 0, pres = 0;
+    int64_t prow = 0, pc0 = 0;
+    uint64_t pcc = 0;                        // per-chunk counts, 16 bits each
+    uint32_t ptot = 0, pres = 0;
     int par = 0;
     auto finish = [&](int pb) {
         uint32_t base = 0;
-        bool fits = pcnt <= STCAP;
-        if (fits && pcnt) {
+        bool fits = ptot <= GCAP;
+        if (fits && ptot) {
             base = __shfl(pres, 0, WAVE);
-            fits = (int64_t)base + pcnt <= ws.cap;
+            fits = (int64_t)base + ptot <= ws.cap;
         }
-        if (lane == 0) {
-            ws.tab[pc * n + prow] = make_uint2(base, fits ? pcnt : 0u);
-            if (!fits) atomicOr(&ws.flags[prow], F_OVERFLOW);
+        if (lane < FGS && pc0 + lane < C) {
+            uint32_t off = 0, cc = 0;
+#pragma unroll
+            for (int u = 0; u < FGS; ++u) {
+                const uint32_t cu = (uint32_t)(pcc >> (16 * u)) & 0xFFFFu;
+                off += u < lane ? cu : 0u;
+                cc = u == lane ? cu : cc;
+            }
+            ws.tab[(pc0 + lane) * n + prow] = make_uint2(base + off, fits ? cc : 0u);
         }
+        if (!fits && lane == 0) atomicOr(&ws.flags[prow], F_OVERFLOW);
         if (fits) {
             const uint32_t* si = st_idx[pb][wv];
             const float* sv = st_val[pb][wv];
             uint32_t* oi = ws.ent_idx + prow * ws.cap + base;
             float* ov = ws.ent_val + prow * ws.cap + base;
-            // fixed trip count (STCAP / 64 predicated slots): the compiler's vmcnt bookkeeping
+            // fixed trip count (GCAP / 64 predicated slots): the compiler's vmcnt bookkeeping
             // stays exact for the loads in flight behind these stores
 #pragma unroll
-            for (int k = 0; k < STCAP / 64; ++k) {
+            for (int k = 0; k < GCAP / 64; ++k) {
                 const uint32_t e = (uint32_t)(k * 64 + lane);
-                if (e < pcnt) { oi[e] = si[e]; ov[e] = sv[e]; }
+                if (e < ptot) { oi[e] = si[e]; ov[e] = sv[e]; }
             }
         }
     };
     while (it < items) {
-        const int64_t c = it - row * C;
-        const int64_t j0 = c * CHUNK;
         const uint32_t T = sload(ws.thr + row);
-        const uint32_t lim = (uint32_t)min((int64_t)CHUNK, d - j0);     // valid elements in this chunk
         const int64_t nit = it + stride;
-        const int64_t nrow = nit < items ? nit / C : row;
-        const auto rsn = nit < items ? chunk_rsrc(rows.row_s(nrow), (nit - nrow * C) * CHUNK, d)
-                                     : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
         uint32_t* si = st_idx[par][wv];
         float* sv = st_val[par][wv];
-        uint32_t cnt = 0;
-        // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
-        // component) index constants out of the item loop into 64 live VGPRs
-        uint32_t lb = (uint32_t)lane * 4u;
-        asm volatile("" : "+v"(lb));
+        uint32_t cnt = 0;                    // entries in this group so far
+        uint64_t ccp = 0;
+        const int64_t cg0 = c;
+        int64_t nrow = row, nc = c;
+        // straight-line over the group, no early exit: the chunks of a row's short last group
+        // past the row end have lim 0 and empty descriptors (their loads return zeros), so the
+        // compiler's vmcnt bookkeeping stays exact from one group's atomic to its use
 #pragma unroll
-        for (int L = 0; L < 16; ++L) {
-            const int P = L + RING - 1;
-            ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
-            const float4 x = ring[L % RING];
-            const uint32_t jl = lb + (uint32_t)(L * 256);                 // offset inside the chunk
-            const float vq[4] = {x.x, x.y, x.z, x.w};
+        for (int sub = 0; sub < FGS; ++sub, ++c) {
+            const int64_t j0 = c * CHUNK;
+            const uint32_t lim = (uint32_t)max((int64_t)0, min((int64_t)CHUNK, d - j0));  // valid elements
+            // descriptor of the chunk after this one (same group, else the next item's first)
+            __amdgpu_buffer_rsrc_t rsn;
+            if (sub + 1 < FGS) {
+                rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
+            } else if (nit < items) {
+                nrow = nit / G;
+                nc = (nit - nrow * G) * FGS;
+                rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
+            } else {
+                rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
+            }
+            const uint32_t cnt0 = cnt;
+            // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
+            // component) index constants out of the loop into 64 live VGPRs
+            uint32_t lb = (uint32_t)lane * 4u;
+            asm volatile("" : "+v"(lb));
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const bool f = (jl + q < lim) && mag_key(vq[q]) >= T;
-                const uint64_t m = __ballot(f);
-                if (m) {
-                    const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
-                    if (f && pos < STCAP) { si[pos] = (uint32_t)j0 + jl + q; sv[pos] = vq[q]; }
-                    cnt += (uint32_t)__popcll(m);
+            for (int L = 0; L < 16; ++L) {
+                const int P = L + RING - 1;
+                ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
+                const float4 x = ring[L % RING];
+                const uint32_t jl = lb + (uint32_t)(L * 256);             // offset inside the chunk
+                const float vq[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool f = (jl + q < lim) && mag_key(vq[q]) >= T;
+                    const uint64_t m = __ballot(f);
+                    if (m) {
+                        const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                        if (f && pos < GCAP) { si[pos] = (uint32_t)j0 + jl + q; sv[pos] = vq[q]; }
+                        cnt += (uint32_t)__popcll(m);
+                    }
                 }
             }
+            ccp |= (uint64_t)min(cnt - cnt0, 0xFFFFu) << (16 * (c - cg0));
+            rs = rsn;
         }
         if (pv) finish(par ^ 1);
         uint32_t res = 0;
-        if (cnt && cnt <= STCAP && lane == 0) res = atomicAdd(&ws.rowcnt[row], cnt);
-        pv = true; prow = row; pc = c; pcnt = cnt; pres = res;
-        // this chunk's staging writes before next-next chunk's reuse of the buffer are ordered by
+        if (cnt && cnt <= GCAP && lane == 0) res = atomicAdd(&ws.rowcnt[row], cnt);
+        pv = true; prow = row; pc0 = cg0; pcc = ccp; ptot = cnt; pres = res;
+        // the staging writes of this group and the copy-out reads of the buffer's next use are in
         // the wave's own program order; the fence keeps the compiler from moving LDS ops across
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         par ^= 1;
         it = nit;
         row = nrow;
-        rs = rsn;
+        c = nc;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     finish(par ^ 1);
@@ -756,27 +788,21 @@ static int grid_stride_blocks(int64_t items, int64_t cap = 4096) {
 }
 
 // Runs the TopK / RandK pipeline for n rows and writes out (ASSIGN: n == 1 dense encode).
-static int filter_ring() {
-    static const int r = [] {
-        const char* e = getenv("FLC_FILTER_RING");
-        return (e && atoi(e) == 16) ? 16 : 8;
+static int filter_group() {
+    static const int g = [] {
+        const char* e = getenv("FLC_FILTER_GS");     // tuning runs only
+        return (e && atoi(e) == 2) ? 2 : 4;
     }();
-    return r;
+    return g;
 }
 
-template <int RING>
+template <int FGS>
 static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream_t st) {
-    static int resident = 0;
-    if (!resident) {
-        int dev = 0, cus = 0, per = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_topk_filter_fast<RING>, 256, 0);
-        resident = std::max(1, cus * std::max(1, per));
-    }
-    const int64_t waves = n * nchunks(d);
-    const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, resident));
-    hipLaunchKernelGGL((k_topk_filter_fast<RING>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+    // oversubscribed grid (measured: 8-16 K blocks beat a resident-only persistent grid by ~5 %,
+    // the hardware dispatcher balances the tail)
+    const int64_t waves = n * ((nchunks(d) + FGS - 1) / FGS);
+    const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 16384));
+    hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
 }
 
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
@@ -815,8 +841,8 @@ hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, 
             { ProfScope _ps("k_topk_filter", st);
             // persistent grid: exactly the resident blocks (a second partial wave of blocks would
             // leave the chip half idle at the end); buffer loads need no 16 B row alignment
-            if (filter_ring() == 8) launch_filter<8>(rows, n, d, ws, st);
-            else launch_filter<16>(rows, n, d, ws, st); }
+            if (filter_group() == 2) launch_filter<2>(rows, n, d, ws, st);
+            else launch_filter<4>(rows, n, d, ws, st); }
             FLC_CHECK_LAUNCH("k_topk_filter");
             const int64_t hb = (ws.cap + 65535) / 65536;
             for (int p = 0; p < 3; ++p) {
