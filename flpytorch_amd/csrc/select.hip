@@ -135,25 +135,107 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
         double rr = ks + 4.0 * sqrt(ks) + 8.0;
         rank = (uint32_t)min((double)S, ceil(rr));
     }
-    uint32_t prefix = 0, krem = rank;
-    for (int p = 0; p < 3; ++p) {
-        for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
-        __syncthreads();
-        for (int i = threadIdx.x; i < S; i += 256) {
-            uint32_t k = keys[i];
-            if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
+    // key of sample rank r (from the top): three 11/11/9-bit passes over the LDS sample
+    auto rank_key = [&](uint32_t r) {
+        uint32_t prefix = 0, krem = r;
+        for (int p = 0; p < 3; ++p) {
+            for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
+            __syncthreads();
+            for (int i = threadIdx.x; i < S; i += 256) {
+                uint32_t k = keys[i];
+                if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
+            }
+            __syncthreads();
+            uint32_t bin, above;
+            hist_find(h, krem, bin, above, scratch);
+            prefix = (prefix << pass_bits(p)) | bin;
+            krem -= above;
+            __syncthreads();
         }
-        __syncthreads();
-        uint32_t bin, above;
-        hist_find(h, krem, bin, above, scratch);
-        prefix = (prefix << pass_bits(p)) | bin;
-        krem -= above;
-        __syncthreads();
-    }
+        return prefix;
+    };
+    const uint32_t tkey = rank_key(rank);
+    // estimate of the K-th key (sample rank ks): sizes the first digit of k_cand_select
+    const uint32_t kest = (S == d) ? tkey
+                                   : rank_key((uint32_t)max(1.0, min((double)S, (double)K * (double)S / (double)d)));
     if (threadIdx.x == 0) {
-        ws.thr[row] = (rank >= (uint32_t)S && S != d) ? 0u : prefix;
+        ws.thr[row] = (rank >= (uint32_t)S && S != d) ? 0u : tkey;
+        ws.prefix[row] = kest;
         ws.flags[row] = 0;
         ws.rowcnt[row] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Exact K-th key over a row's candidate list (fast path), one workgroup per row.
+// Every candidate has key >= T (the sample threshold), and the K-th largest key of the row is
+// among them when the list holds >= K entries.  Digits are taken of the offset dk = key - T:
+// the first digit is dk >> s0 clamped to HBINS-1, with s0 sized so that the sample's estimate of
+// the K-th key falls in the lowest quarter of the bins; the following digits are 11-bit slices
+// of dk below s0 (usually one, exact: 2 passes over the list instead of 3 full-key passes, and
+// the bins spread over the populated range instead of the few exponent values a full-key first
+// digit sees).  A K-th key in the clamp bin (estimate off by > 4x) sends the row to the exact
+// path.  Result as k_radix_select's last pass: thr = K-th key, krem = ties to admit, F_TIES when
+// the list has more keys equal to thr than that.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    for (int64_t row = blockIdx.x; row < n; row += gridDim.x) {
+        if (ws.flags[row]) continue;                                     // overflowed in the filter
+        const uint32_t cnt = ws.rowcnt[row];
+        if (cnt < (uint32_t)K) {                                          // sample threshold too high
+            if (threadIdx.x == 0) ws.flags[row] |= F_SHORT;
+            continue;
+        }
+        const uint32_t T = ws.thr[row];
+        const uint32_t span = ws.prefix[row] - T;                         // kest >= T
+        int s = 0;
+        while (s < 21 && (((uint64_t)span * 4u) >> s) >= (uint64_t)HBINS) ++s;
+        const float* vals = ws.ent_val + row * ws.cap;                    // cap % 4 == 0: 16 B rows
+        const float4* v4 = reinterpret_cast<const float4*>(vals);
+        const uint32_t n4 = cnt >> 2;
+        uint32_t prefix = 0, krem = (uint32_t)K, last = 0;
+        bool first = true, fail = false;
+        int sh = s;
+        while (true) {
+            const int s1 = first ? sh : max(0, sh - 11);
+            const uint32_t mask = first ? 0xFFFFFFFFu : ((1u << (sh - s1)) - 1u);
+            for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
+            __syncthreads();
+            auto add = [&](float x) {
+                const uint32_t dk = mag_key(x) - T;
+                if (first) atomicAdd(&h[min(dk >> s1, (uint32_t)(HBINS - 1))], 1u);
+                else if ((dk >> sh) == prefix) atomicAdd(&h[(dk >> s1) & mask], 1u);
+            };
+            for (uint32_t i = threadIdx.x; i < n4; i += 256) {
+                const float4 q = v4[i];
+                add(q.x); add(q.y); add(q.z); add(q.w);
+            }
+            for (uint32_t i = n4 * 4 + threadIdx.x; i < cnt; i += 256) add(vals[i]);
+            __syncthreads();
+            uint32_t bin, above;
+            hist_find(h, krem, bin, above, scratch);
+            last = h[bin];
+            if (first && bin == HBINS - 1) { fail = true; break; }
+            prefix = first ? bin : ((prefix << (sh - s1)) | bin);
+            krem -= above;
+            sh = s1;
+            first = false;
+            __syncthreads();
+            if (sh == 0) break;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (fail) {
+                ws.flags[row] |= F_SHORT;
+            } else {
+                ws.thr[row] = T + prefix;
+                ws.krem[row] = krem;
+                if (last > krem) ws.flags[row] |= F_TIES;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -746,7 +828,8 @@ int64_t sel_capacity(int codec, int64_t d, int64_t K) {
     if (codec == FLC_RANDK) return std::max<int64_t>(K, 1);
     // candidates of the fast path (~K (1 + 4/sqrt(ks))) with margin; the exact path needs K + CHUNK
     int64_t cap = 2 * K + 2 * CHUNK;
-    return std::min<int64_t>(std::max<int64_t>(cap, 1), std::max<int64_t>(d, 1));
+    cap = std::min<int64_t>(std::max<int64_t>(cap, 1), std::max<int64_t>(d, 1));
+    return (cap + 3) & ~int64_t(3);        // rows of the candidate lists start 16 B aligned
 }
 
 static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, size_t* bytes) {
@@ -844,14 +927,9 @@ hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, 
             if (filter_group() == 2) launch_filter<2>(rows, n, d, ws, st);
             else launch_filter<4>(rows, n, d, ws, st); }
             FLC_CHECK_LAUNCH("k_topk_filter");
-            const int64_t hb = (ws.cap + 65535) / 65536;
-            for (int p = 0; p < 3; ++p) {
-                { ProfScope _ps("k_radix_hist", st);
-hipLaunchKernelGGL((k_radix_hist<false>), dim3(grid_stride_blocks(n * hb)), dim3(256), 0, st, rows, n, d, p, ws); }
-                FLC_CHECK_LAUNCH("k_radix_hist");
-                hipLaunchKernelGGL((k_radix_select<false>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, p, K, ws);
-                FLC_CHECK_LAUNCH("k_radix_select");
-            }
+            { ProfScope _ps("k_cand_select", st);
+            hipLaunchKernelGGL(k_cand_select, dim3(grid_stride_blocks(n, 8192)), dim3(256), 0, st, n, K, ws); }
+            FLC_CHECK_LAUNCH("k_cand_select");
             // ambiguous ties at the K-th magnitude stay on the fast path: tie prefix per chunk
             hipLaunchKernelGGL(k_cand_tie_count, dim3(grid_stride_blocks(n * bpr, 4096)), dim3(256), 0, st, n, d, ws);
             FLC_CHECK_LAUNCH("k_cand_tie_count");
