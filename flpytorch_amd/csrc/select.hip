@@ -27,6 +27,7 @@ constexpr uint32_t ALL = 0xFFFFFFFFu;
 constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
 constexpr int SMAX = 16384;          // sample size kept in LDS
 constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
+constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
 
 struct SelWs {            // carved from the caller workspace
     uint2* tab;           // [C][N] (offset, count) of each row's entries in chunk c
@@ -37,7 +38,8 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* thr;        // [N] admission key: entries with key >= thr are summed
     uint32_t* prefix;     // [N] radix-select state
     uint32_t* krem;       // [N]
-    uint32_t* tieprefix;  // [C][N] ties (key == thr) in chunks before c   (fallback only)
+    uint32_t* tieprefix;  // [C][N] ties (key == thr) in chunks before c   (exact path only)
+    uint32_t* tiecut;     // [N] fast path, F_TIES: largest element index admitted among key == thr
     uint32_t* hist;       // [N][HBINS]
     uint32_t* worklist;   // [N] rows on the exact path
     uint32_t* nwork;      // [1]
@@ -226,13 +228,36 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
             if (sh == 0) break;
         }
         __syncthreads();
+        // ambiguous ties (more entries with key == thr than places left): the reference keeps the
+        // lowest indices (torch.topk on CPU; oracle.codecs.topk_indices).  Gather the tie indices
+        // and find the krem-th smallest: the admission cut for k_chunk_accum.
+        const uint32_t thr = T + prefix;
+        bool ties = !fail && last > krem;
+        if (ties && last > TIECAP) { fail = true; ties = false; }      // pathological: exact path
+        if (ties) {
+            uint32_t* tix = h;                                           // reuse the histogram
+            if (threadIdx.x == 0) scratch[0] = 0;
+            __syncthreads();
+            const uint32_t* idxs = ws.ent_idx + row * ws.cap;
+            for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+                if (mag_key(vals[i]) == thr) tix[atomicAdd(&scratch[0], 1u)] = idxs[i];
+            }
+            __syncthreads();
+            const uint32_t m = scratch[0];                              // == last
+            for (uint32_t a = threadIdx.x; a < m; a += 256) {
+                const uint32_t ia = tix[a];
+                uint32_t rank = 0;
+                for (uint32_t b = 0; b < m; ++b) rank += tix[b] < ia ? 1u : 0u;
+                if (rank == krem - 1) ws.tiecut[row] = ia;              // indices are distinct
+            }
+        }
         if (threadIdx.x == 0) {
             if (fail) {
                 ws.flags[row] |= F_SHORT;
             } else {
-                ws.thr[row] = T + prefix;
+                ws.thr[row] = thr;
                 ws.krem[row] = krem;
-                if (last > krem) ws.flags[row] |= F_TIES;
+                if (ties) ws.flags[row] |= F_TIES;
             }
         }
         __syncthreads();
@@ -636,29 +661,10 @@ __global__ __launch_bounds__(256) void k_tie_count(RowSrc rows, int64_t n, int64
     }
 }
 
-// Fast path, ambiguous ties: per chunk count of key == thr in the chunk's candidate list.
-__global__ __launch_bounds__(256) void k_cand_tie_count(int64_t n, int64_t d, SelWs ws) {
-    const int64_t C = nchunks(d);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t bpr = (C + 3) / 4;
-    for (int64_t it = blockIdx.x; it < n * bpr; it += gridDim.x) {
-        const int64_t row = it / bpr;
-        if ((ws.flags[row] & (F_TIES | F_EXACT)) != F_TIES) continue;
-        const int64_t c = (it % bpr) * 4 + wv;
-        if (c >= C) continue;
-        const uint2 te = ws.tab[c * n + row];
-        const uint32_t T = ws.thr[row];
-        uint32_t cnt = 0;
-        for (uint32_t e = lane; e < te.y; e += 64) cnt += (mag_key(ws.ent_val[row * ws.cap + te.x + e]) == T) ? 1u : 0u;
-        cnt = wave_sum(cnt);
-        if (lane == 0) ws.tieprefix[c * n + row] = cnt;
-    }
-}
-
-// Exclusive prefix of the per-chunk tie counts, in chunk (= index) order, for the rows that
-// need it: EXACT=false -> fast-path rows with ambiguous ties, true -> the exact-path worklist.
-template <bool EXACT>
+// Exclusive prefix of the per-chunk tie counts, in chunk (= index) order, for the exact-path
+// worklist rows.
 __global__ __launch_bounds__(256) void k_tie_scan(int64_t n, int64_t d, SelWs ws) {
+    constexpr bool EXACT = true;
     __shared__ uint32_t part[256];
     const int64_t C = nchunks(d);
     const int64_t nrows = EXACT ? (int64_t)(*ws.nwork) : n;
@@ -718,6 +724,7 @@ __global__ __launch_bounds__(64) void k_randk_scan(int64_t n, int64_t d, SelWs w
         run += v;
     }
     ws.thr[row] = 0;
+    ws.flags[row] = F_EXACT;      // the list holds exactly the kept entries: k_chunk_accum admits all
     ws.rowcnt[row] = run;
 }
 
@@ -740,81 +747,139 @@ __global__ __launch_bounds__(256) void k_randk_scatter(RowSrc rows, int64_t n, i
 // ASSIGN (single row, no weights): out = tile with the entry values stored, not added
 // (keeps -0.0 like torch's out[ind] = x[ind]).
 // ------------------------------------------------------------------------------------------
-// Tie admission on the fast path (row flag F_TIES without F_EXACT): among the entries whose key
-// equals the K-th magnitude T, only the `need` lowest indices are summed.  rank = ties in the
-// row's earlier chunks (tieprefix) + ties of this chunk's list with a smaller index.  Taken only
-// for key == T entries of such rows (a handful per row).
-__device__ inline bool tie_admitted(const SelWs& ws, int64_t row, int64_t c, int64_t n, uint32_t off, uint32_t cnt,
-                                    uint32_t T, uint32_t idx) {
-    uint32_t rank = ws.tieprefix[c * n + row];
-    const uint32_t* li = ws.ent_idx + row * ws.cap + off;
-    const float* lv = ws.ent_val + row * ws.cap + off;
-    for (uint32_t e = 0; e < cnt; ++e) rank += (mag_key(lv[e]) == T && li[e] < idx) ? 1u : 0u;
-    return rank < ws.krem[row];
+// Admission per entry: exact-path rows (F_EXACT) hold exactly their admitted entries; fast-path
+// rows admit key > thr, and key == thr either all (no F_TIES) or up to the row's tie cut (the
+// largest index admitted among the ties, k_cand_select).
+//
+// One wave owns one chunk: a 4096-float LDS tile into which the rows are folded in row order
+// (bit-exact sequential sum; within a row the entries' columns are distinct).  The walk over the
+// N rows is a software pipeline: the per-row state (tab entry, thr, cut, mode, weight) of 64 rows
+// is fetched one batch ahead with lane = row, and the entry lists of the next AP rows are in
+// flight while a row is folded (a ring of AP register slots, 2 x 64 entries per row), so the
+// wave never waits on a dependent tab -> entries round trip.
+// ------------------------------------------------------------------------------------------
+constexpr int AP = 8;                      // rows of entry lists in flight
+
+struct RowMeta {
+    uint2 te;          // (offset, count) of the row's list in this chunk
+    uint32_t thr, cut, mode;
+    float w;
+};
+
+__device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64_t r, const float* w) {
+    RowMeta m;
+    m.te = make_uint2(0, 0);
+    m.thr = 0; m.cut = 0xFFFFFFFFu; m.mode = 0; m.w = 1.f;
+    if (r < n) {
+        m.te = ws.tab[c * n + r];
+        m.thr = ws.thr[r];
+        const uint32_t f = ws.flags[r];
+        m.mode = (f & F_EXACT) ? 2u : ((f & F_TIES) ? 1u : 0u);
+        if (m.mode == 1u) m.cut = ws.tiecut[r];
+        if (w) m.w = w[r];
+    }
+    return m;
+}
+
+__device__ inline __amdgpu_buffer_rsrc_t list_rsrc(const void* p, uint32_t cnt) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(cnt * 4u), 0x00020000);
 }
 
 template <bool ASSIGN>
 __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
                                                      float wt, float* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) float tile[4][CHUNK];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t C = nchunks(d);
     float* tl = tile[wv];
-    constexpr int PF = 16;                 // rows whose first 64 entries are in flight together
+    const int64_t nb = (n + 63) / 64;                  // row batches
     for (int64_t c = (int64_t)blockIdx.x * 4 + wv; c < C; c += (int64_t)gridDim.x * 4) {
-        // waves are independent: each owns its tile, LDS ops of one wave retire in order
         for (int i = lane; i < CHUNK; i += 64) tl[i] = 0.f;
-        const int64_t cbase = c * CHUNK;
-        for (int64_t i0 = 0; i0 < n; i0 += PF) {
-            // lanes 0..PF-1 fetch the per-row state of rows i0..i0+PF-1
-            uint2 te = make_uint2(0, 0);
-            uint32_t tthr = 0, ttie = 0;
-            float tw = 1.f;
-            if (lane < PF && i0 + lane < n) {
-                te = ws.tab[c * n + i0 + lane];
-                tthr = ws.thr[i0 + lane];
-                ttie = (ws.flags[i0 + lane] & (F_TIES | F_EXACT)) == F_TIES;
-                tw = w ? w[i0 + lane] : 1.f;
-            }
-            uint32_t e_idx[PF];
-            float e_val[PF];
+        const uint32_t cbase = (uint32_t)(c * CHUNK);
+        RowMeta cur = load_meta(ws, c, n, lane, w), nxt;
+        // ring of AP rows' entries (the first 128 of each list; range-checked buffer loads, lanes
+        // past the list end get index ~0 = no column)
+        uint32_t ri[AP][2];
+        float rv[AP][2];
+        auto fetch = [&](const RowMeta& m, int q, int64_t row, int slot) {
+            const uint32_t off = __builtin_amdgcn_readlane(m.te.x, q), cnt = __builtin_amdgcn_readlane(m.te.y, q);
+            const auto di = list_rsrc(ws.ent_idx + row * ws.cap + off, cnt);
+            const auto dv = list_rsrc(ws.ent_val + row * ws.cap + off, cnt);
 #pragma unroll
-            for (int q = 0; q < PF; ++q) {
-                const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
-                e_idx[q] = 0;
-                e_val[q] = 0.f;
-                if ((uint32_t)lane < cnt && i0 + q < n) {
-                    e_idx[q] = ws.ent_idx[(i0 + q) * ws.cap + off + lane];
-                    e_val[q] = ws.ent_val[(i0 + q) * ws.cap + off + lane];
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t e = (uint32_t)lane + 64u * h;
+                const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(di, lane * 4, h * 256, 0);
+                ri[slot][h] = e < cnt ? x : 0xFFFFFFFFu;
+                rv[slot][h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dv, lane * 4, h * 256, 0));
+            }
+        };
+        auto fold = [&](uint32_t ix, float vv, uint32_t T, uint32_t cut, uint32_t mode, float wi) {
+            const uint32_t loc = ix - cbase;                   // ~0 index: loc >= CHUNK
+            const uint32_t key = mag_key(vv);
+            if (loc < (uint32_t)CHUNK && (mode == 2u || key > T || (key == T && ix <= cut))) {
+                if (ASSIGN) tl[loc] = vv;
+                else tl[loc] = tl[loc] + wi * vv;
+            }
+        };
+#pragma unroll
+        for (int q = 0; q < AP; ++q) fetch(cur, q, q, q);
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t i0 = b * 64;
+            nxt = load_meta(ws, c, n, i0 + 64 + lane, w);    // next batch's state, one batch ahead
+            if (__builtin_expect(__ballot(cur.te.y > 128u) == 0ull, 1)) {
+                // every list of the batch fits the ring slots: straight-line pipeline
+#pragma unroll
+                for (int q = 0; q < 64; ++q) {
+                    const int slot = q % AP;
+                    const uint32_t T = __builtin_amdgcn_readlane(cur.thr, q);
+                    const uint32_t cut = __builtin_amdgcn_readlane(cur.cut, q);
+                    const uint32_t mode = __builtin_amdgcn_readlane(cur.mode, q);
+                    const float wi = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.w), q));
+                    fold(ri[slot][0], rv[slot][0], T, cut, mode, wi);
+                    fold(ri[slot][1], rv[slot][1], T, cut, mode, wi);
+                    if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, slot);
+                    else fetch(nxt, q + AP - 64, i0 + q + AP, slot);   // past n: empty lists
                 }
-            }
+            } else {
+                // some list is longer than 128 entries: the same walk with the tails folded in place
+                for (int q = 0; q < 64; ++q) {
+                    const int slot = q % AP;
+                    const uint32_t T = __shfl(cur.thr, q, WAVE), cut = __shfl(cur.cut, q, WAVE);
+                    const uint32_t mode = __shfl(cur.mode, q, WAVE), cnt = __shfl(cur.te.y, q, WAVE);
+                    const uint32_t off = __shfl(cur.te.x, q, WAVE);
+                    const float wi = __shfl(cur.w, q, WAVE);
+                    uint32_t i_0 = 0, i_1 = 0;
+                    float v_0 = 0.f, v_1 = 0.f;
 #pragma unroll
-            for (int q = 0; q < PF; ++q) {
-                if (i0 + q >= n) break;
-                const int64_t row = i0 + q;
-                const uint32_t off = __shfl(te.x, q, WAVE), cnt = __shfl(te.y, q, WAVE);
-                const uint32_t T = __shfl(tthr, q, WAVE);
-                const bool tiemode = __shfl(ttie, q, WAVE) != 0;
-                const float wi = __shfl(tw, q, WAVE);
-                for (uint32_t e0 = 0; e0 < cnt; e0 += 64) {
-                    const uint32_t e = e0 + lane;
-                    if (e >= cnt) continue;
-                    uint32_t ix;
-                    float vv;
-                    if (e0 == 0) { ix = e_idx[q]; vv = e_val[q]; }          // prefetched
-                    else { ix = ws.ent_idx[row * ws.cap + off + e]; vv = ws.ent_val[row * ws.cap + off + e]; }
-                    const uint32_t key = mag_key(vv);
-                    bool ok = key >= T;
-                    if (tiemode && key == T) ok = tie_admitted(ws, row, c, n, off, cnt, T, ix);
-                    if (ok) {
-                        const int loc = (int)(ix - (uint32_t)cbase);
-                        if (ASSIGN) tl[loc] = vv;
-                        else tl[loc] = tl[loc] + wi * vv;
+                    for (int z = 0; z < AP; ++z)
+                        if (z == slot) { i_0 = ri[z][0]; i_1 = ri[z][1]; v_0 = rv[z][0]; v_1 = rv[z][1]; }
+                    fold(i_0, v_0, T, cut, mode, wi);
+                    fold(i_1, v_1, T, cut, mode, wi);
+                    const int64_t row = i0 + q;
+                    for (uint32_t e = 128u + lane; e < cnt; e += 64)
+                        fold(ws.ent_idx[row * ws.cap + off + e], ws.ent_val[row * ws.cap + off + e], T, cut, mode, wi);
+                    // refill the slot (same contract as the straight-line path)
+                    const RowMeta& m = (q + AP < 64) ? cur : nxt;
+                    const int qq = (q + AP) & 63;
+                    const uint32_t offn = __shfl(m.te.x, qq, WAVE), cntn = __shfl(m.te.y, qq, WAVE);
+                    const int64_t rown = i0 + q + AP;
+                    uint32_t xi[2];
+                    float xv[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t e = (uint32_t)lane + 64u * h;
+                        xi[h] = e < cntn ? ws.ent_idx[rown * ws.cap + offn + e] : 0xFFFFFFFFu;
+                        xv[h] = e < cntn ? ws.ent_val[rown * ws.cap + offn + e] : 0.f;
                     }
+#pragma unroll
+                    for (int z = 0; z < AP; ++z)
+                        if (z == slot) { ri[z][0] = xi[0]; ri[z][1] = xi[1]; rv[z][0] = xv[0]; rv[z][1] = xv[1]; }
                 }
             }
+            cur = nxt;
         }
-        const int64_t len = min((int64_t)CHUNK, d - cbase);
+        const int64_t len = min((int64_t)CHUNK, d - (int64_t)cbase);
         for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
     }
 }
@@ -849,10 +914,12 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     s.nwork = cv.take<uint32_t>(4);
     if (codec == FLC_TOPK) {
         s.tieprefix = cv.take<uint32_t>((size_t)C * nn);
+        s.tiecut = cv.take<uint32_t>(nn);
         s.hist = cv.take<uint32_t>((size_t)nn * HBINS);
         s.cursor = nullptr;
     } else {
         s.tieprefix = nullptr;
+        s.tiecut = nullptr;
         s.hist = nullptr;
         s.cursor = cv.take<uint32_t>((size_t)C * nn);
     }
@@ -930,11 +997,6 @@ hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, 
             { ProfScope _ps("k_cand_select", st);
             hipLaunchKernelGGL(k_cand_select, dim3(grid_stride_blocks(n, 8192)), dim3(256), 0, st, n, K, ws); }
             FLC_CHECK_LAUNCH("k_cand_select");
-            // ambiguous ties at the K-th magnitude stay on the fast path: tie prefix per chunk
-            hipLaunchKernelGGL(k_cand_tie_count, dim3(grid_stride_blocks(n * bpr, 4096)), dim3(256), 0, st, n, d, ws);
-            FLC_CHECK_LAUNCH("k_cand_tie_count");
-            hipLaunchKernelGGL((k_tie_scan<false>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, d, ws);
-            FLC_CHECK_LAUNCH("k_tie_scan");
         } else {
             FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
         }
@@ -951,7 +1013,7 @@ hipLaunchKernelGGL((k_radix_hist<true>), dim3(grid_stride_blocks(n * hb)), dim3(
         }
         hipLaunchKernelGGL(k_tie_count, dim3(grid_stride_blocks(n * bpr, 4096)), dim3(256), 0, st, rows, n, d, ws);
         FLC_CHECK_LAUNCH("k_tie_count");
-        hipLaunchKernelGGL((k_tie_scan<true>), dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, d, ws);
+        hipLaunchKernelGGL(k_tie_scan, dim3(grid_stride_blocks(n, 1024)), dim3(256), 0, st, n, d, ws);
         FLC_CHECK_LAUNCH("k_tie_scan");
         int gb = grid_stride_blocks(n * bpr, 8192);
         { ProfScope _ps("k_topk_filter_exact", st);
@@ -961,7 +1023,7 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
-    const int ab = grid_stride_blocks((C + 3) / 4, 2048);
+    const int ab = grid_stride_blocks((C + 3) / 4, 4096);
     { ProfScope _ps("k_chunk_accum", st);
 if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
     else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out); }
