@@ -122,10 +122,14 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
     } else {
         const int P = SMAX / 256;
         S = SMAX;
-        for (int i = threadIdx.x; i < S; i += 256) {
-            int p = i >> 8, q = i & 255;
-            int64_t off = ((int64_t)p * (d - 256)) / (P - 1);
-            keys[i] = mag_key(r[off + q]);
+        // piece p = 256 contiguous elements at p (d - 256) / (P - 1); thread t reads element t of
+        // 8 pieces per round trip
+        for (int p0 = 0; p0 < P; p0 += 8) {
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = r[((int64_t)(p0 + u) * (d - 256)) / (P - 1) + threadIdx.x];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) keys[(p0 + u) * 256 + threadIdx.x] = mag_key(x[u]);
         }
     }
     // rank (from the top) of the sample element whose key is the threshold
@@ -210,7 +214,16 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
                 if (first) atomicAdd(&h[min(dk >> s1, (uint32_t)(HBINS - 1))], 1u);
                 else if ((dk >> sh) == prefix) atomicAdd(&h[(dk >> s1) & mask], 1u);
             };
-            for (uint32_t i = threadIdx.x; i < n4; i += 256) {
+            // 8 float4 per thread in flight per round trip (the walk is latency-bound otherwise)
+            uint32_t i = threadIdx.x;
+            for (; i + 7 * 256 < n4; i += 8 * 256) {
+                float4 q[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) q[u] = v4[i + u * 256];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) { add(q[u].x); add(q[u].y); add(q[u].z); add(q[u].w); }
+            }
+            for (; i < n4; i += 256) {
                 const float4 q = v4[i];
                 add(q.x); add(q.y); add(q.z); add(q.w);
             }
@@ -239,7 +252,14 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
             if (threadIdx.x == 0) scratch[0] = 0;
             __syncthreads();
             const uint32_t* idxs = ws.ent_idx + row * ws.cap;
-            for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+            for (uint32_t i = threadIdx.x; i < n4; i += 256) {
+                const float4 q = v4[i];
+                const float qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (mag_key(qv[u]) == thr) tix[atomicAdd(&scratch[0], 1u)] = idxs[i * 4 + u];
+            }
+            for (uint32_t i = n4 * 4 + threadIdx.x; i < cnt; i += 256) {
                 if (mag_key(vals[i]) == thr) tix[atomicAdd(&scratch[0], 1u)] = idxs[i];
             }
             __syncthreads();
