@@ -9,7 +9,10 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libflcodec.so")
+# FLC_LIB_VARIANT=<tag> loads flpytorch_amd/libflcodec_<tag>.so instead (A/B tuning runs of two
+# builds in one process tree on one box; tools/ab_build.sh makes them).
+LIB_PATH = os.path.join(_HERE, "libflcodec%s.so" % (
+    ("_" + os.environ["FLC_LIB_VARIANT"]) if os.environ.get("FLC_LIB_VARIANT") else ""))
 
 FLC_OK, FLC_ERR_ARG, FLC_ERR_DTYPE, FLC_ERR_HIP, FLC_ERR_WORKSPACE, FLC_ERR_UNSUPPORTED = range(6)
 FLC_IDENT, FLC_LAZY, FLC_RANDK, FLC_NATURAL, FLC_STD_DITHERING, FLC_NAT_DITHERING, FLC_TOPK = range(1, 8)

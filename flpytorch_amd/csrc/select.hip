@@ -27,13 +27,17 @@ constexpr uint32_t ALL = 0xFFFFFFFFu;
 constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
 constexpr int SMAX = 16384;          // sample size kept in LDS
 constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
+// Row counters of the candidate lists are reserved with atomics by every wave; counters of
+// neighbouring rows sharing an L2 line serialise those atomics (measured: -10 % filter bandwidth,
+// tools/probe_filter.hip), so each row's counter has a 128 B line of its own.
+constexpr int RCS = 32;
 constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
 
 struct SelWs {            // carved from the caller workspace
     uint2* tab;           // [C][N] (offset, count) of each row's entries in chunk c
     uint32_t* ent_idx;    // [N][cap] element index within the row
     float* ent_val;       // [N][cap] entry value (already scaled for RandK)
-    uint32_t* rowcnt;     // [N] entries used
+    uint32_t* rowcnt;     // [N * RCS] entries used (one counter per 128 B line)
     uint32_t* flags;      // [N]
     uint32_t* thr;        // [N] admission key: entries with key >= thr are summed
     uint32_t* prefix;     // [N] radix-select state
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
         ws.thr[row] = (rank >= (uint32_t)S && S != d) ? 0u : tkey;
         ws.prefix[row] = kest;
         ws.flags[row] = 0;
-        ws.rowcnt[row] = 0;
+        ws.rowcnt[(row) * RCS] = 0;
     }
 }
 
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
     __shared__ uint32_t scratch[260];
     for (int64_t row = blockIdx.x; row < n; row += gridDim.x) {
         if (ws.flags[row]) continue;                                     // overflowed in the filter
-        const uint32_t cnt = ws.rowcnt[row];
+        const uint32_t cnt = ws.rowcnt[(row) * RCS];
         if (cnt < (uint32_t)K) {                                          // sample threshold too high
             if (threadIdx.x == 0) ws.flags[row] |= F_SHORT;
             continue;
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
         }
         cnt = wave_sum(cnt);
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&ws.rowcnt[row], cnt);
+        if (lane == 0) base = atomicAdd(&ws.rowcnt[(row) * RCS], cnt);
         base = __shfl(base, 0, WAVE);
         const bool fits = (int64_t)base + cnt <= ws.cap;
         if (lane == 0) {
@@ -553,7 +557,7 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
         }
         if (pv) finish(par ^ 1);
         uint32_t res = 0;
-        if (cnt && cnt <= GCAP && lane == 0) res = atomicAdd(&ws.rowcnt[row], cnt);
+        if (cnt && cnt <= GCAP && lane == 0) res = atomicAdd(&ws.rowcnt[(row) * RCS], cnt);
         pv = true; prow = row; pc0 = cg0; pcc = ccp; ptot = cnt; pres = res;
         // the staging writes of this group and the copy-out reads of the buffer's next use are in
         // the wave's own program order; the fence keeps the compiler from moving LDS ops across
@@ -583,7 +587,7 @@ __global__ __launch_bounds__(256) void k_radix_hist(RowSrc rows, int64_t n, int6
         const int64_t li = it / bpr;
         const int64_t row = FULLROW ? (int64_t)ws.worklist[li] : li;
         if (!FULLROW && ws.flags[row]) continue;
-        const int64_t len = FULLROW ? d : (int64_t)ws.rowcnt[row];
+        const int64_t len = FULLROW ? d : (int64_t)ws.rowcnt[(row) * RCS];
         const int64_t b0 = (it % bpr) * BLK;
         if (b0 >= len) continue;
         const int64_t b1 = min(len, b0 + BLK);
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(256) void k_radix_select(int64_t n, int p, int64_t 
         const int64_t row = FULLROW ? (int64_t)ws.worklist[li] : li;
         if (!FULLROW && ws.flags[row]) continue;
         uint32_t* gh = ws.hist + row * HBINS;
-        if (!FULLROW && p == 0 && ws.rowcnt[row] < (uint32_t)K) {   // sample threshold too high
+        if (!FULLROW && p == 0 && ws.rowcnt[(row) * RCS] < (uint32_t)K) {   // sample threshold too high
             for (int i = threadIdx.x; i < HBINS; i += 256) gh[i] = 0;
             if (threadIdx.x == 0) ws.flags[row] |= F_SHORT;
             continue;
@@ -650,7 +654,7 @@ __global__ void k_build_worklist(int64_t n, int64_t K, int64_t d, SelWs ws, int 
             uint32_t pos = atomicAdd(&cnt, 1u);
             ws.worklist[pos] = (uint32_t)row;
             ws.flags[row] = F_EXACT;
-            ws.rowcnt[row] = 0;
+            ws.rowcnt[(row) * RCS] = 0;
             ws.prefix[row] = 0;
         }
     }
@@ -745,7 +749,7 @@ __global__ __launch_bounds__(64) void k_randk_scan(int64_t n, int64_t d, SelWs w
     }
     ws.thr[row] = 0;
     ws.flags[row] = F_EXACT;      // the list holds exactly the kept entries: k_chunk_accum admits all
-    ws.rowcnt[row] = run;
+    ws.rowcnt[(row) * RCS] = run;
 }
 
 __global__ __launch_bounds__(256) void k_randk_scatter(RowSrc rows, int64_t n, int64_t d, int64_t K, flc_pattern pat,
@@ -925,7 +929,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     s.tab = cv.take<uint2>((size_t)C * nn);
     s.ent_idx = cv.take<uint32_t>((size_t)nn * s.cap);
     s.ent_val = cv.take<float>((size_t)nn * s.cap);
-    s.rowcnt = cv.take<uint32_t>(nn);
+    s.rowcnt = cv.take<uint32_t>((size_t)nn * RCS);
     s.flags = cv.take<uint32_t>(nn);
     s.thr = cv.take<uint32_t>(nn);
     s.prefix = cv.take<uint32_t>(nn);
@@ -968,10 +972,10 @@ static int filter_group() {
 
 template <int FGS>
 static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream_t st) {
-    // oversubscribed grid (measured: 8-16 K blocks beat a resident-only persistent grid by ~5 %,
+    // oversubscribed grid (measured: 16-32 K blocks beat a resident-only persistent grid by ~5 %,
     // the hardware dispatcher balances the tail)
     const int64_t waves = n * ((nchunks(d) + FGS - 1) / FGS);
-    const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 16384));
+    const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 32768));
     hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
 }
 
