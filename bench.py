@@ -40,11 +40,14 @@ sys.path.insert(0, ROOT)
 PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
 
 WORKLOADS = {
-    "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2),
-    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_scatter", config=1),
-    "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ew_accum_vec", config=3),
+    "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2,
+               others=["k_topk_sample", "k_cand_select", "k_chunk_accum"]),
+    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_scatter", config=1, others=["k_chunk_accum"]),
+    # sparse QSGD path (dither_sparse.hip): one read of every row in k_ds_filter
+    "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3,
+               others=["k_ds_sample", "k_ds_accum"]),
     # the serverGradient fold alone (identity codec), C4's shard shape
-    "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3),
+    "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3, others=[]),
 }
 
 
@@ -60,7 +63,7 @@ def kernel_bytes(kernel, n, d, k):
         return 8 * n * k            # gather K values per row + write K (idx, value) entries
     if kernel in ("k_ew_accum_vec", "k_reduce_vec"):
         return 4 * n * d + 4 * d    # read every row once, write the [D] result
-    return 4 * n * d                # k_topk_filter: read every row once
+    return 4 * n * d                # k_topk_filter / k_ds_filter: read every row once
 
 
 def cpu_baseline(spec, d, budget_s=12.0):
@@ -214,7 +217,8 @@ def main():
     if world > 1:
         dist.barrier()
     _lib.profile_enable(True)
-    _lib.profile_collect(wl["kernel"])          # drop anything recorded before the timed region
+    for kname in [wl["kernel"]] + wl["others"]:
+        _lib.profile_collect(kname)             # drop anything recorded before the timed region
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -225,6 +229,11 @@ def main():
     elapsed = time.perf_counter() - t0
     _lib.profile_enable(False)
     kms, klaunch = _lib.profile_collect(wl["kernel"])
+    others = {}
+    for kname in wl["others"]:
+        oms, on = _lib.profile_collect(kname)
+        if on:
+            others[kname] = round(oms / on, 4)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -264,7 +273,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": wl["kernel"],
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBS, 4) if achieved else None, "traffic": traffic,
-                         "bytes_per_launch": kb, "avg_launch_ms": round(kavg_ms, 4), "launches": klaunch},
+                         "bytes_per_launch": kb, "avg_launch_ms": round(kavg_ms, 4), "launches": klaunch,
+                         "other_kernels_avg_ms": others},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

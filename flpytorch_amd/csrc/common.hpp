@@ -87,6 +87,10 @@ int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st);
+bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d);
+size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d, const float* w,
+           float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st);
 int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out,
                 hipStream_t st);
 
@@ -123,12 +127,27 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
     return h;
 }
-// u(client, j) = fmix32(colbase(j) ^ rowkey(client)): the column base is a fixed hash of the
-// element index (computed once per column by the kernels, outside the client loop), the row key
-// a 32-bit fold of the client key; the outer fmix32 fully avalanches their xor.
+// u(client, j) = hi8 << 24 | lo24 from two hashes keyed by the row key rk (a 32-bit fold of the
+// client key):
+//   lo24 = fmix32(colbase(j) ^ rk) >> 8   — the column base is a fixed hash of the element index,
+//          computed once per column by the tile-owner kernels, outside the client loop;
+//   hi8  = byte (j & 3) of grouphash(j >> 2, rk) = fmix32((j >> 2) * 0x9E3779B1 + rk) — one hash
+//          serves 4 consecutive elements.
+// The split lets a streaming pass decide `u >= t` for a small t from the top byte alone, at a
+// quarter hash per element (the sparse QSGD candidate filter, dither_sparse.hip).
 __host__ __device__ inline uint32_t colbase(uint32_t j) { return fmix32(j * 0x9E3779B1u + 0x7F4A7C15u); }
 __host__ __device__ inline uint32_t rowkey(uint64_t ckey) { return (uint32_t)(ckey >> 32) ^ (uint32_t)ckey; }
-__host__ __device__ inline uint32_t dev_u32(uint64_t ckey, uint32_t j) { return fmix32(colbase(j) ^ rowkey(ckey)); }
+__host__ __device__ inline uint32_t grouphash(uint32_t g, uint32_t rk) { return fmix32(g * 0x9E3779B1u + rk); }
+__host__ __device__ inline uint32_t draw_join(uint32_t hg, uint32_t q, uint32_t lo) {
+    return ((hg >> (8u * q)) << 24) | (lo >> 8);
+}
+__host__ __device__ inline uint32_t dev_draw(uint32_t cs, uint32_t hg, uint32_t j, uint32_t rk) {
+    return draw_join(hg, j & 3u, fmix32(cs ^ rk));
+}
+__host__ __device__ inline uint32_t dev_u32(uint64_t ckey, uint32_t j) {
+    const uint32_t rk = rowkey(ckey);
+    return dev_draw(colbase(j), grouphash(j >> 2, rk), j, rk);
+}
 // Decision for a draw h (u = h * 2^-32) against an fp32 probability p:  h < sat_u32(ceil(p*2^32)).
 // Equals (u < p) exactly for p in [0, 1); p >= 1 admits every h but 0xFFFFFFFF (prob. 2^-32), and
 // p <= 0 or NaN admits none.  ldexp / ceil / saturating convert are exact single instructions.

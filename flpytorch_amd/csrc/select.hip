@@ -19,7 +19,7 @@
 //                    distinct within a row, so every element sees its terms in row order).
 //
 // Keys: |x| bits with the sign cleared (uint32, monotone; NaN above inf like torch.topk).
-#include "common.hpp"
+#include "chunks.hpp"
 
 namespace flc {
 
@@ -27,10 +27,6 @@ constexpr uint32_t ALL = 0xFFFFFFFFu;
 constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
 constexpr int SMAX = 16384;          // sample size kept in LDS
 constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
-// Row counters of the candidate lists are reserved with atomics by every wave; counters of
-// neighbouring rows sharing an L2 line serialise those atomics (measured: -10 % filter bandwidth,
-// tools/probe_filter.hip), so each row's counter has a 128 B line of its own.
-constexpr int RCS = 32;
 constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
 
 struct SelWs {            // carved from the caller workspace
@@ -51,7 +47,6 @@ struct SelWs {            // carved from the caller workspace
     int64_t cap;
 };
 
-__host__ __device__ inline int64_t nchunks(int64_t d) { return (d + CHUNK - 1) >> CHUNK_SHIFT; }
 
 // ------------------------------------------------------------------------------------------
 // Block-level helpers
@@ -426,16 +421,6 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
 constexpr int GCAP = 512;             // staged entries per group (4 chunks: 3.1 %, ~2.5x the mean at 1.2 %; more -> row overflow)
 static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 
-// Buffer descriptor of one chunk built from the wave-uniform chunk base (SGPRs): 32-bit lane
-// offsets, no 64-bit address VGPRs, and the hardware range check returns 0 past the row's end.
-__device__ inline __amdgpu_buffer_rsrc_t chunk_rsrc(const float* r, int64_t j0, int64_t d) {
-    const int64_t len = max((int64_t)0, min((int64_t)CHUNK, d - j0));
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r + j0), (short)0, (int)(len * 4), 0x00020000);
-}
-__device__ inline float4 load_q(__amdgpu_buffer_rsrc_t rs, int lane, int L) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, L * 1024, 0);
-    return make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
-}
 
 // A chunk is 16 wave-loads of 1 KB.  RING float4 registers per lane hold a software pipeline RING-1
 // loads deep (the next chunk's descriptor is built up front; past the last item it has
@@ -805,9 +790,6 @@ __device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64
     return m;
 }
 
-__device__ inline __amdgpu_buffer_rsrc_t list_rsrc(const void* p, uint32_t cnt) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(cnt * 4u), 0x00020000);
-}
 
 template <bool ASSIGN>
 __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,

@@ -1,0 +1,162 @@
+"""GPU parity of the sparse fused dithering path (flpytorch_amd/csrc/dither_sparse.hip).
+
+QSGD / standard dithering with p = 2 in device-RNG mode, fused encode + reduce: one pass per row
+keeps the elements that could be nonzero (against a sampled lower bound of the norm), the chunk
+owners encode them exactly.  Bar: BIT-EXACT (uint32 compare) against the oracle — the reference's
+op order (oracle/codecs.py, compressors.py:270-299) with the device draws restated in numpy
+(oracle/devrng.py) — including the sign of zero, and bit-identical to the dense two-pass path at
+C4 scale.  FLC_DITHER_PATH=sparse|dense forces a path (the automatic choice keeps small D dense).
+"""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import codecs as oc
+from oracle import devrng
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20240607
+
+
+@pytest.fixture(scope="module")
+def ag():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    from flpytorch_amd import aggregation
+    return aggregation
+
+
+def bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.uint32)
+
+
+def assert_bitexact(got, want):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
+    g, w = bits(got), bits(want)
+    # NaN results must sit at the same positions; their payload / sign bit is not compared
+    # (numpy on x86 and the GPU propagate different NaN encodings)
+    same = (g == w) | (np.isnan(np.asarray(got, np.float32)).ravel() & np.isnan(np.asarray(want, np.float32)).ravel())
+    if not same.all():
+        bad = np.nonzero(~same)[0]
+        raise AssertionError(f"{bad.size} of {g.size} elements differ; first {bad[:5]}: "
+                             f"{np.asarray(got).ravel()[bad[:5]]} vs {np.asarray(want).ravel()[bad[:5]]}")
+
+
+def oracle_uplink(spec, rows, client0, weights=None, seed=SEED):
+    d = rows.shape[1]
+    enc, norms = [], []
+    for i in range(rows.shape[0]):
+        o = oc.OracleCompressor(spec, d)
+        o.testp = devrng.uniforms(seed, client0 + i, d)
+        enc.append(o.compress(rows[i]))
+        norms.append(o.norm(rows[i]))
+    return oc.reduce_plain(enc, weights), np.array(norms, dtype=np.float32)
+
+
+def make_rows(kind, n, d, g):
+    if kind == "normal":
+        return g.standard_normal((n, d)).astype(np.float32)
+    if kind == "heavy":      # N(0,1) * 10^U(-3, 3): wide dynamic range
+        return (g.standard_normal((n, d)) * 10.0 ** g.uniform(-3, 3, (n, d))).astype(np.float32)
+    if kind == "sparse":     # mostly exact zeros: the sample sees nothing, the bound is +inf
+        r = np.zeros((n, d), dtype=np.float32)
+        for i in range(n):
+            k = g.choice(d, size=max(1, d // 5000), replace=False)
+            r[i, k] = g.standard_normal(k.size).astype(np.float32)
+        return r
+    if kind == "negative":   # every element < 0 and tiny vs the norm: many -0 columns
+        r = -np.abs(g.standard_normal((n, d))).astype(np.float32) * 1e-3
+        r[:, 0] = -50.0
+        return r
+    if kind == "clustered":  # the mass in one short run: lists overflow -> dense rows
+        r = (g.standard_normal((n, d)) * 1e-4).astype(np.float32)
+        r[:, d // 3: d // 3 + 20000] = g.standard_normal((n, 20000)).astype(np.float32) * 3
+        return r
+    if kind == "ones":       # flat rows: the s sqrt(D) bound is attained
+        return np.sign(g.standard_normal((n, d))).astype(np.float32)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["normal", "heavy", "sparse", "negative", "clustered", "ones"])
+@pytest.mark.parametrize("spec", ["qsgd:4", "qsgd:127"])
+def test_sparse_dither_vs_oracle(ag, monkeypatch, kind, spec):
+    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
+    n, d, client0 = 5, 300_001, 11
+    rows = make_rows(kind, n, d, np.random.default_rng(zlib.crc32(f"{kind}{spec}".encode())))
+    want, wn = oracle_uplink(spec, rows, client0)
+    red = ag.UplinkReducer(ag.initCompressor(spec, d), seed=SEED)
+    pn = torch.empty(n, device="cuda")
+    got = red(torch.from_numpy(rows).cuda(), client0=client0, pnorms_out=pn)
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)
+
+
+@pytest.mark.parametrize("d", [1, 3, 4096, 4097, 8192 * 3 + 5, 16384, 16385, 100_000])
+def test_sparse_dither_shapes(ag, monkeypatch, d):
+    """Chunk / item / sample boundaries, tiny rows (whole-row sample)."""
+    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
+    n, client0 = 3, 0
+    rows = np.random.default_rng(d).standard_normal((n, d)).astype(np.float32)
+    want, _ = oracle_uplink("qsgd:16", rows, client0)
+    red = ag.UplinkReducer(ag.initCompressor("qsgd:16", d), seed=SEED)
+    assert_bitexact(red(torch.from_numpy(rows).cuda(), client0=client0), want)
+    # the pointer-array entry point reads the same rows
+    rt = torch.from_numpy(rows).cuda()
+    assert_bitexact(red([rt[i].clone() for i in range(n)], client0=client0), want)
+
+
+@pytest.mark.parametrize("bad", [None, "nan", "inf"])
+def test_sparse_dither_weights_nonfinite(ag, monkeypatch, bad):
+    """Weights (some negative, one zero) flip zero signs; a row with a NaN (norm NaN: every
+    output NaN, as in the reference) or an inf element (norm inf) is folded dense."""
+    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
+    n, d, client0 = 6, 120_000, 5
+    g = np.random.default_rng(3)
+    rows = make_rows("negative", n, d, g)
+    rows[1] = g.standard_normal(d).astype(np.float32)
+    if bad == "nan":
+        rows[4, 777] = np.nan
+    if bad == "inf":
+        rows[5, 31] = np.inf
+    w = [0.5, -2.0, 1.0, 0.0, 3.0, 1.25]
+    want, _ = oracle_uplink("qsgd:8", rows, client0, weights=w)
+    red = ag.UplinkReducer(ag.initCompressor("qsgd:8", d), seed=SEED)
+    assert_bitexact(red(torch.from_numpy(rows).cuda(), client0=client0, weights=w), want)
+
+
+def test_sparse_equals_dense_c4_scale(ag, monkeypatch):
+    """C4's row length (D = 25 M, qsgd:127): the sparse path and the dense two-pass path give
+    the same bits, and the same norms (the oracle would take minutes at this size)."""
+    n, d = 6, 25_000_000
+    x = torch.empty((n, d), device="cuda").normal_(generator=torch.Generator("cuda").manual_seed(4))
+    red = ag.UplinkReducer(ag.initCompressor("qsgd:127", d), seed=SEED)
+    outs, norms = {}, {}
+    for path in ("sparse", "dense"):
+        monkeypatch.setenv("FLC_DITHER_PATH", path)
+        pn = torch.empty(n, device="cuda")
+        outs[path] = red(x, client0=100, pnorms_out=pn).cpu().numpy()
+        norms[path] = pn.cpu().numpy()
+    assert_bitexact(norms["sparse"], norms["dense"])
+    assert_bitexact(outs["sparse"], outs["dense"])
+    nz = np.count_nonzero(outs["sparse"])
+    assert 0 < nz < d
+
+
+def test_auto_path_choice(ag, monkeypatch):
+    """Without the override, C4's shape takes the sparse path and short rows the dense one
+    (checked through the library's launch profiler)."""
+    from flpytorch_amd import _lib
+    monkeypatch.delenv("FLC_DITHER_PATH", raising=False)
+    for d, want, other in ((25_000_000, "k_ds_filter", "k_ew_accum_vec"), (200_000, "k_ew_accum_vec", "k_ds_filter")):
+        x = torch.randn((2, d), device="cuda")
+        red = ag.UplinkReducer(ag.initCompressor("qsgd:127", d), seed=SEED)
+        _lib.profile_enable(True)
+        try:
+            red(x)
+            torch.cuda.synchronize()
+            assert _lib.profile_collect(want)[1] == 1, (d, want)
+            assert _lib.profile_collect(other)[1] == 0, (d, other)
+        finally:
+            _lib.profile_enable(False)

@@ -16,6 +16,7 @@ import pytest
 import torch
 
 from oracle import codecs as oc
+from oracle import devrng
 from oracle.rng import OracleRandomState
 from tests.golden_io import load
 
@@ -217,7 +218,7 @@ def test_encode_reduce_device_rng(ag, spec):
             assert np.unique(idx).size == o.K and idx.min() >= 0 and idx.max() < d
             o.S = idx
         else:
-            o.testp = np.array([lib.flc_device_uniform(seed, client0 + i, j) for j in range(d)])
+            o.testp = devrng.uniforms(seed, client0 + i, d)
         enc.append(o.compress(rows[i]))
     want = oc.reduce_plain(enc)
     red = ag.UplinkReducer(ag.initCompressor(spec, d), seed=seed)

@@ -117,3 +117,19 @@ def test_device_rng_host_mirror():
     u = np.array([lib.flc_device_uniform(42, 3, j) for j in range(20000)])
     assert u.min() >= 0.0 and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01
     assert math.isclose(np.var(u), 1 / 12, rel_tol=0.03)
+
+
+def test_device_rng_oracle_restatement():
+    """oracle/devrng.py (numpy) states the kernels' draw arithmetic independently; it equals the
+    library's host mirror of the same generator (common.hpp dev_u32) on every index tried."""
+    from oracle import devrng
+    lib = _lib.load()
+    for seed, client in [(42, 3), (0, 0), (2**63 + 5, 10**9), (20240607, 11)]:
+        j = np.concatenate([np.arange(5000), [2**31 - 1, 2**31, 2**32 - 1, 123456789]]).astype(np.int64)
+        got = devrng.dev_u32(seed, client, j.astype(np.uint32)).astype(np.float64) / 2**32
+        ref = np.array([lib.flc_device_uniform(seed, client, int(v)) for v in j])
+        assert np.array_equal(got, ref)
+    # the top byte: one group hash serves the 4 elements of an aligned group, byte (j & 3) each
+    u = devrng.dev_u32(7, 1, np.arange(1 << 16, dtype=np.uint32))
+    top = (u >> np.uint32(24)).astype(np.int64)
+    assert abs(top.mean() - 127.5) < 2.0 and np.unique(top).size == 256

@@ -23,7 +23,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL_SUBSTR = {"c3": "k_topk_filter_fast", "c4": "k_ew_accum_vec", "reduce": "k_reduce_vec",
+KERNEL_SUBSTR = {"c3": "k_topk_filter_fast", "c4": "k_ds_filter", "reduce": "k_reduce_vec",
                  "c2": "k_randk_scatter"}
 
 
