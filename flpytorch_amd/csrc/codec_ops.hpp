@@ -59,7 +59,7 @@ struct UniformSrc {
 };
 
 // the reference's decision `testp < p` (float64 draw vs fp32 p promoted), compressors.py:260, 288.
-// Device mode: h = fmix32(colbase(j) ^ rowkey) against thr32 (common.hpp); p2 = p * 2^32.
+// Device mode: h = dev_draw(colbase(j), grouphash, j, rowkey) against thr32 (common.hpp); p2 = p * 2^32.
 // hg: grouphash(j >> 2, rk), shared by the 4 elements of an aligned group (hg_of below for one
 // element).
 template <bool COMPAT>

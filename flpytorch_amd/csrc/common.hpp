@@ -128,21 +128,21 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
     return h;
 }
 // u(client, j) = hi8 << 24 | lo24 from two hashes keyed by the row key rk (a 32-bit fold of the
-// client key):
-//   lo24 = fmix32(colbase(j) ^ rk) >> 8   — the column base is a fixed hash of the element index,
-//          computed once per column by the tile-owner kernels, outside the client loop;
+// client key), each the MurmurHash3 finaliser of a keyed Weyl sequence:
+//   lo24 = fmix32(colbase(j) + (rk ^ 0x27D4EB2F)) >> 8,  colbase(j) = j * 0x85EBCA77 (computed
+//          once per column by the tile-owner kernels, outside the client loop);
 //   hi8  = byte (j & 3) of grouphash(j >> 2, rk) = fmix32((j >> 2) * 0x9E3779B1 + rk) — one hash
 //          serves 4 consecutive elements.
 // The split lets a streaming pass decide `u >= t` for a small t from the top byte alone, at a
 // quarter hash per element (the sparse QSGD candidate filter, dither_sparse.hip).
-__host__ __device__ inline uint32_t colbase(uint32_t j) { return fmix32(j * 0x9E3779B1u + 0x7F4A7C15u); }
+__host__ __device__ inline uint32_t colbase(uint32_t j) { return j * 0x85EBCA77u; }
 __host__ __device__ inline uint32_t rowkey(uint64_t ckey) { return (uint32_t)(ckey >> 32) ^ (uint32_t)ckey; }
 __host__ __device__ inline uint32_t grouphash(uint32_t g, uint32_t rk) { return fmix32(g * 0x9E3779B1u + rk); }
 __host__ __device__ inline uint32_t draw_join(uint32_t hg, uint32_t q, uint32_t lo) {
     return ((hg >> (8u * q)) << 24) | (lo >> 8);
 }
 __host__ __device__ inline uint32_t dev_draw(uint32_t cs, uint32_t hg, uint32_t j, uint32_t rk) {
-    return draw_join(hg, j & 3u, fmix32(cs ^ rk));
+    return draw_join(hg, j & 3u, fmix32(cs + (rk ^ 0x27D4EB2Fu)));
 }
 __host__ __device__ inline uint32_t dev_u32(uint64_t ckey, uint32_t j) {
     const uint32_t rk = rowkey(ckey);

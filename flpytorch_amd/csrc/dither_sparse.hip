@@ -143,7 +143,6 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
     __shared__ float st_val[2][4][DS_GCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t C = nchunks(d);
     const int64_t G = ws.G;
     const int64_t items = n * G;
@@ -210,7 +209,6 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
 #pragma unroll
         for (int sub = 0; sub < FGS; ++sub, ++c) {
             const int64_t j0 = c * CHUNK;
-            const uint32_t lim = (uint32_t)max((int64_t)0, min((int64_t)CHUNK, d - j0));
             __amdgpu_buffer_rsrc_t rsn;
             if (sub + 1 < FGS) {
                 rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
@@ -222,29 +220,35 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
             }
             const uint32_t cnt0 = cnt;
-            uint32_t lb = (uint32_t)lane * 4u;
-            asm volatile("" : "+v"(lb));
+            // element index of (L, q): jb + 256 L + q (opaque: keeps the 64 constants out of VGPRs)
+            uint32_t jb = (uint32_t)j0 + (uint32_t)lane * 4u;
+            asm volatile("" : "+v"(jb));
             const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;   // hash input of L = 0
 #pragma unroll
             for (int L = 0; L < 16; ++L) {
                 const int P = L + RING - 1;
                 ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
                 const float4 x = ring[L % RING];
-                const uint32_t jl = lb + (uint32_t)(L * 256);
                 const uint32_t hg = fmix32(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     a2 = fma((double)vq[q], (double)vq[q], a2);
                     const float hi = (float)((hg >> (8 * q)) & 0xFFu);
-                    const bool f = (jl + q < lim) && fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
+                    // no range test: past the row end the loads return 0, and a zero candidate
+                    // encodes to 0 (never folded); NaN from 0 * inf (qc = inf) is not a candidate
+                    const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
                     const uint64_t m = __ballot(f);
-                    if (m) {
-                        const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
-                        if (f && pos < DS_GCAP) { si[pos] = (uint32_t)j0 + jl + q; sv[pos] = vq[q]; }
-                        cnt += (uint32_t)__popcll(m);
-                    }
+                    // branch-free compaction: position = cnt + candidates in lower lanes; an item
+                    // past DS_GCAP overflows (its row is folded dense), so wrapping is harmless
+                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (DS_GCAP - 1);
+                    if (f) { si[pos] = jb + (uint32_t)(L * 256 + q); sv[pos] = vq[q]; }
+                    cnt += (uint32_t)__popcll(m);
                 }
+                // keep the norm's fma chain here: left alone, the compiler sinks all 128 of an
+                // item's fmas to its end and holds the 128 x values live (218 VGPRs)
+                asm volatile("" : "+v"(a2));
             }
             ccp |= (uint64_t)min(cnt - cnt0, 0xFFFFu) << (16 * (c - cg0));
             rs = rsn;

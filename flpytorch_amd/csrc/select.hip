@@ -433,7 +433,6 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
     __shared__ float st_val[2][4][GCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t C = nchunks(d);
     const int64_t G = (C + FGS - 1) / FGS;                               // groups per row
     const int64_t items = n * G;
@@ -531,7 +530,8 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
                     const bool f = (jl + q < lim) && mag_key(vq[q]) >= T;
                     const uint64_t m = __ballot(f);
                     if (m) {
-                        const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                        const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt));
                         if (f && pos < GCAP) { si[pos] = (uint32_t)j0 + jl + q; sv[pos] = vq[q]; }
                         cnt += (uint32_t)__popcll(m);
                     }

@@ -8,7 +8,7 @@ device-mode parity tests do not take their expected draws from the product libra
 
     ckey  = mix64(seed ^ mix64(0x9E3779B97F4A7C15 * (client + 1)))      (SplitMix64 finaliser)
     rk    = (ckey >> 32) ^ (ckey & 0xFFFFFFFF)
-    lo    = fmix32(colbase(j) ^ rk),  colbase(j) = fmix32(j * 0x9E3779B1 + 0x7F4A7C15)
+    lo    = fmix32(j * 0x85EBCA77 + (rk ^ 0x27D4EB2F))
     hg    = fmix32((j >> 2) * 0x9E3779B1 + rk)                          (one per 4 elements)
     u32   = (byte (j & 3) of hg) << 24 | lo >> 8,    u = u32 * 2^-32
 """
@@ -46,8 +46,7 @@ def fmix32(h):
 
 
 def colbase(j):
-    j = np.asarray(j, dtype=np.uint32)
-    return fmix32(j * np.uint32(0x9E3779B1) + np.uint32(0x7F4A7C15))
+    return np.asarray(j, dtype=np.uint32) * np.uint32(0x85EBCA77)
 
 
 def grouphash(g, rk):
@@ -60,7 +59,7 @@ def dev_u32(seed, client, j):
     with np.errstate(over="ignore"):
         j = np.asarray(j, dtype=np.uint32)
         rk = rowkey(client_key(seed, client))
-        lo = fmix32(colbase(j) ^ rk)
+        lo = fmix32(colbase(j) + (rk ^ np.uint32(0x27D4EB2F)))
         hg = grouphash(j >> np.uint32(2), rk)
         top = (hg >> (np.uint32(8) * (j & np.uint32(3)))) & np.uint32(0xFF)
         return (top << np.uint32(24)) | (lo >> np.uint32(8))
