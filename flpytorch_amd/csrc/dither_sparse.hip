@@ -22,9 +22,9 @@
 //             DENSE (every element re-read and encoded) if the norm is below n_lo (sample
 //             misjudged), not finite, its weight not finite, or its list overflowed.
 //   accum   : one wave owns a 4096-element chunk as an fp32 LDS tile and folds the rows in order:
-//             each candidate is encoded exactly (DitherOp, the dense path's functor) and nonzero
-//             contributions are added; untouched columns get the sign of zero the sequential fold
-//             of the all-zero contributions gives (-0 only if every row contributes -0).
+//             each candidate is encoded exactly (ds_encode = DitherOp::apply's arithmetic) and
+//             nonzero contributions are added; untouched columns get the sign of zero the
+//             sequential fold of the all-zero contributions gives (-0 only if every row gives -0).
 //
 // The candidate test is conservative (never drops a nonzero).  For n >= n_lo, in the first level
 // interval [0, l1] the encode keeps l0 = 0 iff  h < ceil(p 2^32),  p = RN(RN(y - l1) / (-l1)),
@@ -37,29 +37,31 @@
 
 namespace flc {
 
-constexpr uint32_t DS_DENSE = 1u, DS_OVER = 2u;
-constexpr int DS_FGS = 2;                  // chunks per filter work item (8192 elements)
+constexpr uint32_t DS_DENSE = 1u, DS_FAST = 4u;
+constexpr int DS_FGS = 2;                  // chunks per filter work item (8192 elements; default)
 constexpr int DS_GCAP = 512;               // staged candidates per item (6.25 %; more -> row overflow)
 constexpr int DS_SMAX = 16384;             // sample elements per row
-constexpr uint32_t DS_SENT = 0x7FBADBADu;  // LDS tile: untouched column (a signalling NaN: never computed)
 constexpr float DS_QT = 254.98f;
 constexpr int DS_MAXS = 512;               // level table entries kept in LDS by the fold
-static_assert(DS_GCAP % 64 == 0, "copy-out runs in whole wave slots");
 
 struct DsWs {
-    uint2* tab;           // [C][N] (offset, count) of each row's candidates in chunk c
-    uint32_t* ent_idx;    // [N][cap] element index within the row
-    float* ent_val;       // [N][cap] x
-    uint32_t* rowcnt;     // [N * RCS] entries used
+    uint2* tab;           // [H][N] (offset, count) of each row's candidates in half chunk h
+    uint2* ent;           // [N][cap] (entry word, x bits); word = chunk-local index (12 bits) |
+                          // the draw's top byte << 12
+    uint32_t* ovfi;       // [N][G] 1: the item overflowed its staging capacity
     uint32_t* flags;      // [N] DS_*
     float* qc;            // [N] candidate scale
     float* nlo;           // [N] norm lower bound the scale assumes
     double* partial;      // [N][G] per-item sums of squares
     float* pn;            // [N] norm
+    float* rpn;           // [N] RN(1 / norm)
     uint32_t* rk;         // [N] device-RNG row key
-    int64_t cap;
+    int64_t cap;          // per row: G * GCAP (each filter item owns a fixed region)
     int64_t G;            // filter items per row
 };
+
+constexpr int HCHUNK = CHUNK / 2;          // the fold's tile: 2048 elements (8 KB of LDS per wave)
+__host__ __device__ inline int64_t nhalves(int64_t d) { return (d + HCHUNK - 1) / HCHUNK; }
 
 // ------------------------------------------------------------------------------------------
 // Sample: one workgroup per row.
@@ -125,31 +127,40 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
         ws.qc[row] = qc;
         ws.nlo[row] = nlof;
         ws.flags[row] = bad ? DS_DENSE : 0u;
-        ws.rowcnt[row * RCS] = 0;
         ws.rk[row] = rowkey(client_key(seed, client0 + row));
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// Filter: the TopK fast filter's structure (select.hip k_topk_filter_fast: RING-deep buffer-load
-// pipeline across chunks and items, wave-private double-buffered LDS staging, one reservation
-// atomic per item consumed an item later) with the dithering candidate test and the norm.
+// Filter: a RING-deep buffer-load pipeline across chunks and items (select.hip's TopK filter
+// structure), the dithering candidate test and the norm.  A work item is DS_FGS consecutive
+// 4096-element chunks of one row; its candidates are compacted (ballot / mbcnt) into wave-private
+// LDS and copied out coalesced into the item's FIXED region of the row's list (item * GCAP): no
+// reservation atomic, so nothing returning sits in the in-order vmcnt queue of the load stream.
+// The tab gets one (offset, count) per 2048-element half chunk (the fold's tile).
 // ------------------------------------------------------------------------------------------
-template <int RING>
+// PROBE (tuning runs only, FLC_DS_PROBE): 0 full; 1 no norm; 2 no candidate test (norm only);
+// 3 loads only (a running xor keeps them alive); 4 full but no copy-out of the staged entries;
+// 5 copy-out into one fixed per-wave scratch region (L2-resident: stores without HBM traffic);
+// 6 full with non-temporal copy-out stores
+template <int RING, int GCAP, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64_t d, DsWs ws) {
     constexpr int FGS = DS_FGS;
+    constexpr int NH = 2 * FGS;                               // half chunks per item
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
-    __shared__ uint32_t st_idx[2][4][DS_GCAP];
-    __shared__ float st_val[2][4][DS_GCAP];
+    static_assert(GCAP % 128 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
+    constexpr int DS_ITEM_STORES = 3 + GCAP / 128;          // partial, overflow, tab, copy-out
+    __shared__ uint2 stage[4][GCAP];                         // (entry word, x bits)
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t C = nchunks(d);
+    const int64_t H = nhalves(d);
     const int64_t G = ws.G;
     const int64_t items = n * G;
     const int64_t stride = (int64_t)gridDim.x * 4;
     int64_t it = (int64_t)blockIdx.x * 4 + wv;
     if (it >= items) return;
     const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
+    uint2* sg = stage[wv];
     float4 ring[RING];
     int64_t row = it / G;
     int64_t c = (it - row * G) * FGS;
@@ -159,52 +170,22 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
         ring[L] = load_q(rs, lane, L);
         __builtin_amdgcn_sched_barrier(0);
     }
-    bool pv = false;
-    int64_t prow = 0, pc0 = 0;
-    uint64_t pcc = 0;
-    uint32_t ptot = 0, pres = 0;
-    int par = 0;
-    auto finish = [&](int pb) {
-        uint32_t base = 0;
-        bool fits = ptot <= DS_GCAP;
-        if (fits && ptot) {
-            base = __shfl(pres, 0, WAVE);
-            fits = (int64_t)base + ptot <= ws.cap;
-        }
-        if (lane < FGS && pc0 + lane < C) {
-            uint32_t off = 0, cc = 0;
+    {
+        // the stores an item ends with, dropped (num_records 0): the loop is entered with the same
+        // vmcnt queue shape as it is re-entered
+        const auto nd = __builtin_amdgcn_make_buffer_rsrc(ws.ent, (short)0, 0, 0x00020000);
 #pragma unroll
-            for (int u = 0; u < FGS; ++u) {
-                const uint32_t cu = (uint32_t)(pcc >> (16 * u)) & 0xFFFFu;
-                off += u < lane ? cu : 0u;
-                cc = u == lane ? cu : cc;
-            }
-            ws.tab[(pc0 + lane) * n + prow] = make_uint2(base + off, fits ? cc : 0u);
-        }
-        if (!fits && lane == 0) atomicOr(&ws.flags[prow], DS_OVER);
-        if (fits) {
-            const uint32_t* si = st_idx[pb][wv];
-            const float* sv = st_val[pb][wv];
-            uint32_t* oi = ws.ent_idx + prow * ws.cap + base;
-            float* ov = ws.ent_val + prow * ws.cap + base;
-#pragma unroll
-            for (int k = 0; k < DS_GCAP / 64; ++k) {
-                const uint32_t e = (uint32_t)(k * 64 + lane);
-                if (e < ptot) { oi[e] = si[e]; ov[e] = sv[e]; }
-            }
-        }
-    };
+        for (int k = 0; k < DS_ITEM_STORES; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, nd, lane * 4, k * 256, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     while (it < items) {
         const float qc = sload(ws.qc + row);
         const uint32_t rk = sload(ws.rk + row);
         const int64_t gi = it - row * G;
         const int64_t nit = it + stride;
-        uint32_t* si = st_idx[par][wv];
-        float* sv = st_val[par][wv];
         uint32_t cnt = 0;
-        uint64_t ccp = 0;
+        uint32_t hc[NH];                                      // running count at each half's end
         double a2 = 0.0;
-        const int64_t cg0 = c;
         int64_t nrow = row, nc = c;
 #pragma unroll
         for (int sub = 0; sub < FGS; ++sub, ++c) {
@@ -219,9 +200,9 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
             } else {
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
             }
-            const uint32_t cnt0 = cnt;
-            // element index of (L, q): jb + 256 L + q (opaque: keeps the 64 constants out of VGPRs)
-            uint32_t jb = (uint32_t)j0 + (uint32_t)lane * 4u;
+            // chunk-local index of (L, q): 4 lane + 256 L + q (opaque: keeps the 64 constants out
+            // of VGPRs); the entry word is that index | the draw's top byte << 12 (ds_encode)
+            uint32_t jb = (uint32_t)lane * 4u;
             asm volatile("" : "+v"(jb));
             const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;   // hash input of L = 0
 #pragma unroll
@@ -233,40 +214,75 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    a2 = fma((double)vq[q], (double)vq[q], a2);
+                    if (PROBE == 0 || PROBE == 2) a2 = fma((double)vq[q], (double)vq[q], a2);
+                    if (PROBE == 3) { a2 = __longlong_as_double(__double_as_longlong(a2) ^ __float_as_uint(vq[q])); continue; }
+                    if (PROBE == 2) continue;
                     const float hi = (float)((hg >> (8 * q)) & 0xFFu);
                     // no range test: past the row end the loads return 0, and a zero candidate
                     // encodes to 0 (never folded); NaN from 0 * inf (qc = inf) is not a candidate
                     const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
                     const uint64_t m = __ballot(f);
-                    // branch-free compaction: position = cnt + candidates in lower lanes; an item
-                    // past DS_GCAP overflows (its row is folded dense), so wrapping is harmless
+                    // position = cnt + candidates in lower lanes; an item past GCAP overflows (its
+                    // row is folded dense), so wrapping is harmless
                     const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (DS_GCAP - 1);
-                    if (f) { si[pos] = jb + (uint32_t)(L * 256 + q); sv[pos] = vq[q]; }
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
+                    if (f) {
+                        const uint32_t word = ((((hg >> (8 * q)) & 0xFFu) << 12) | jb) + (uint32_t)(L * 256 + q);
+                        sg[pos] = make_uint2(word, __float_as_uint(vq[q]));
+                    }
                     cnt += (uint32_t)__popcll(m);
                 }
                 // keep the norm's fma chain here: left alone, the compiler sinks all 128 of an
                 // item's fmas to its end and holds the 128 x values live (218 VGPRs)
                 asm volatile("" : "+v"(a2));
+                if (L == 7) hc[2 * sub] = cnt;
+                if (L == 15) hc[2 * sub + 1] = cnt;
             }
-            ccp |= (uint64_t)min(cnt - cnt0, 0xFFFFu) << (16 * (c - cg0));
             rs = rsn;
         }
         a2 = wave_sum(a2);                                   // fixed butterfly: deterministic
-        if (lane == 0) ws.partial[row * G + gi] = a2;
-        if (pv) finish(par ^ 1);
-        uint32_t res = 0;
-        if (cnt && cnt <= DS_GCAP && lane == 0) res = atomicAdd(&ws.rowcnt[row * RCS], cnt);
-        pv = true; prow = row; pc0 = cg0; pcc = ccp; ptot = cnt; pres = res;
+        const bool fits = cnt <= GCAP;
+        const uint32_t base = (uint32_t)gi * GCAP;
+        // The item's stores: a FIXED sequence of DS_ITEM_STORES vector-memory ops with no exec
+        // branch (every lane stores; duplicate lanes write equal values to equal addresses; the
+        // entry copy-out is range-checked by its buffer descriptor).  The stores sit in the
+        // in-order vmcnt queue in front of the loads issued after them; with one fixed sequence on
+        // every path (the prologue issues the same count of dropped stores) the compiler's static
+        // vmcnt waits count them exactly instead of draining part of the ring.
+        ws.partial[row * G + gi] = a2;
+        ws.ovfi[row * G + gi] = fits ? 0u : 1u;
+        {
+            const int u = lane & (NH - 1);
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int v = 0; v < NH; ++v) {
+                lo = v + 1 == u ? hc[v] : lo;
+                hi = v == u ? hc[v] : hi;
+            }
+            // halves past the row end land in the tab's padding rows (G * NH >= H)
+            ws.tab[(gi * NH + u) * n + row] = make_uint2(base + lo, fits ? hi - lo : 0u);
+        }
+        {
+            // two entries per lane per 16-B store; an odd count's last slot carries a stale entry
+            const uint32_t nrec = fits && PROBE != 4 ? ((cnt + 1u) & ~1u) * 8u : 0u;
+            uint2* dst = ws.ent + row * ws.cap + base;
+            if (PROBE == 5) dst = ws.ent + (((int64_t)blockIdx.x * 4 + wv) % 4096) * GCAP;
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nrec, 0x00020000);
+            const uint4* sq = reinterpret_cast<const uint4*>(sg);
+#pragma unroll
+            for (int k = 0; k < GCAP / 128; ++k) {
+                const uint4 v = sq[k * 64 + lane];
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od, (k * 64 + lane) * 16, 0,
+                    PROBE == 6 ? 2 : 0);
+            }
+        }
+        // the copy-out reads precede the next item's staging writes in the wave's program order
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        par ^= 1;
         it = nit;
         row = nrow;
         c = nc;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    finish(par ^ 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -278,15 +294,19 @@ __global__ __launch_bounds__(256) void k_ds_final(int64_t n, DsWs ws, const floa
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
     double a = 0.0;
-    for (int64_t k = lane; k < ws.G; k += 64) a += ws.partial[row * ws.G + k];
+    uint32_t ov = 0;
+    for (int64_t k = lane; k < ws.G; k += 64) { a += ws.partial[row * ws.G + k]; ov |= ws.ovfi[row * ws.G + k]; }
     a = wave_sum(a);
+    ov = __ballot(ov != 0u) != 0ull;
     if (lane == 0) {
         const float nv = (float)sqrt(a);
         ws.pn[row] = nv;
         if (pnorm_out) pnorm_out[row] = nv;
+        ws.rpn[row] = 1.0f / nv;
         uint32_t fl = ws.flags[row];
         const bool wbad = w && !(fabsf(w[row]) <= 3.4028235e38f);
-        if (!(nv >= ws.nlo[row]) || !(nv <= 3.4028235e38f) || (fl & DS_OVER) || wbad) fl |= DS_DENSE;
+        if (!(nv >= ws.nlo[row]) || !(nv <= 3.4028235e38f) || ov || wbad) fl |= DS_DENSE;
+        if (nv >= 0x1p-40f && nv <= 0x1p80f) fl |= DS_FAST;   // |x| / norm may use div_fast
         ws.flags[row] = fl;
     }
 }
@@ -296,128 +316,222 @@ __global__ __launch_bounds__(256) void k_ds_final(int64_t n, DsWs ws, const floa
 // (first 128 entries from a ring of AP rows in flight, the rest read in place) or, for DENSE rows,
 // the chunk of x itself.  Contributions are W ? w_i * C(x)_j : C(x)_j with C the exact encode.
 // ------------------------------------------------------------------------------------------
-constexpr int DS_AP = 8;
+constexpr int DS_AP = 8;                   // default rows of entry lists in flight (FLC_DS_AP: 8/16/32)
 
 struct DsMeta {
     uint2 te;
-    float pn, w;
+    float pn, rpn, w;
     uint32_t rk, mode;
 };
 
 __device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r, const float* w) {
     DsMeta m;
     m.te = make_uint2(0, 0);
-    m.pn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
+    m.pn = 1.f; m.rpn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
     if (r < n) {
-        m.te = ws.tab[c * n + r];
+        m.te = ws.tab[c * n + r];           // c: half-chunk index
         m.pn = ws.pn[r];
+        m.rpn = ws.rpn[r];
         m.rk = ws.rk[r];
-        m.mode = ws.flags[r] & DS_DENSE;
+        m.mode = ws.flags[r];
         if (w) m.w = w[r];
     }
     return m;
 }
 
-template <bool W>
+// Row state of the exact encode (wave-uniform).
+struct DsRow {
+    float n, rn;          // norm, RN(1 / norm)
+    uint32_t rk2;         // row key of the low draw: rk ^ 0x27D4EB2F (common.hpp dev_draw)
+    bool fast;            // norm inside the div_fast window
+};
+
+// C(x)_j of standard dithering (compressors.py:270-299) for one element, exactly as
+// DitherOp::apply<false> (codec_ops.hpp) computes it, specialised for the sparse fold: the draw's
+// top byte comes with the entry (hi8), and the rare slow cases (|x| or a level gap outside the
+// fast-division window, the interval guess off by one) are taken behind wave-level branches
+// instead of being if-converted.
+template <bool NOTAB = false>
+__device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow& r, const float4* tab, int s,
+                                  float sf) {
+    const float ax = fabsf(x);
+    FastDiv dn;
+    dn.b = r.n; dn.rb = r.rn; dn.ok = true;
+    float y = div_fast(ax, dn);                                   // |x| / pnorm
+    const bool slow = !(r.fast && (ax >= 0x1p-80f || ax == 0.f) && ax <= 0x1p80f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) y = ax / r.n;
+    }
+    int g = (int)(y * sf);                                        // y >= 0; NaN -> 0
+    g = g > s - 1 ? s - 1 : g;
+    float4 t = NOTAB ? make_float4((float)g, (float)g + 1.f, -0x1p-32f, -0x1p32f) : tab[g];
+    const bool off = (y < t.x) | (y > t.y);
+    if (__builtin_expect(__ballot(off) != 0ull, 0)) {            // std levels RN(k/s): at most one off
+        if (off) {
+            g = (y < t.x) ? (g > 0 ? g - 1 : 0) : (g < s - 1 ? g + 1 : g);
+            t = tab[g];
+        }
+    }
+    const bool in = y <= t.y;                                     // y > 1 or NaN: no interval -> 0
+    const float num = y - t.y;
+    FastDiv dd;
+    dd.b = t.z; dd.rb = t.w; dd.ok = true;
+    float p2 = div_fast(num, dd);                                 // p * 2^32
+    const bool gap_slow = t.w == 0.f;                             // gap outside the window (load_table)
+    if (__builtin_expect(__ballot(gap_slow) != 0ull, 0)) {
+        if (gap_slow) p2 = num / t.z;
+    }
+    uint32_t thr;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(thr) : "v"(ceilf(p2)));   // saturating: thr32(p)
+    // draw h = hi8 << 24 | lo24 against thr: the top byte decides unless it equals thr's (1 in
+    // 256), so the low hash is computed only for those lanes
+    const uint32_t th = thr >> 24;
+    bool down = hi8 < th;
+    const bool tie = hi8 == th;
+    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
+        if (tie) down = ((hi8 << 24) | (fmix32(colbase(j) + r.rk2) >> 8)) < thr;
+    }
+    const float lev = in ? (down ? t.x : t.y) : 0.f;
+    return (x == 0.f) ? 0.f : copysignf(lev, x) * r.n;           // (lev * sign(x)) * pnorm
+}
+
+__device__ inline uint32_t ds_hi8(uint32_t j, uint32_t rk) { return (grouphash(j >> 2, rk) >> (8u * (j & 3u))) & 0xFFu; }
+
+// APROBE (tuning runs only, FLC_DS_APROBE; outputs invalid): 1 no encode (t = x); 2 no tile adds;
+// 3 encode without the level-table lookup; 4 no list fetch (constant in-range entries)
+template <bool W, int AP, int APROBE = 0>
 __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_t d, DsWs ws,
                                                   const float* __restrict__ levels, int s,
                                                   const float* __restrict__ w, float wt, float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float tile[4][CHUNK];
+    static_assert(64 % AP == 0, "row groups tile the 64-row batch");
+    __shared__ __attribute__((aligned(16))) float tile[4][HCHUNK];
     __shared__ __attribute__((aligned(16))) float4 tab[DS_MAXS];
-    const bool tab_ok = load_table(levels, s, tab);
+    load_table(levels, s, tab);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t C = nchunks(d);
+    const int64_t H = nhalves(d);
     float* tl = tile[wv];
     const int64_t nb = (n + 63) / 64;
-    DitherOp<false, false> op;
-    op.us = UniformSrc{nullptr, 0};
-    op.rt = RowTabs{nullptr, nullptr, nullptr, nullptr};
-    op.s = s;
-    op.sf = (float)s;
-    op.urow = nullptr;
-    op.fast = false;
-    op.tab_ok = tab_ok;
-    for (int64_t c = (int64_t)blockIdx.x * 4 + wv; c < C; c += (int64_t)gridDim.x * 4) {
-        for (int i = lane; i < CHUNK; i += 64) tl[i] = __uint_as_float(DS_SENT);
-        const uint32_t cbase = (uint32_t)(c * CHUNK);
-        const int64_t len = min((int64_t)CHUNK, d - (int64_t)cbase);
-        DsMeta cur = ds_meta(ws, c, n, lane, w), nxt;
-        uint32_t ri[DS_AP][2];
-        float rv[DS_AP][2];
+    const float sf = (float)s;
+    for (int64_t h = (int64_t)blockIdx.x * 4 + wv; h < H; h += (int64_t)gridDim.x * 4) {
+        // The tile starts at -0.0: (-0) + t == t for every nonzero t, and a column that received a
+        // nonzero contribution never returns to -0 (x + y == -0 needs two -0 addends), so a final
+        // -0 bit pattern marks exactly the untouched columns.  Zero contributions are not added.
+        // Adds are read-modify-writes of the wave's own tile, in row order (one wave executes its
+        // LDS operations in program order; the lanes of one instruction hit distinct columns), so
+        // each column sees its rows' terms in row order.  (ds_add_f32 atomics measured 30 % slower.)
+        for (int i = lane; i < HCHUNK; i += 64) tl[i] = -0.f;
+        const uint32_t hbase = (uint32_t)(h * HCHUNK);
+        const int64_t len = min((int64_t)HCHUNK, d - (int64_t)hbase);
+        DsMeta cur = ds_meta(ws, h, n, lane, w), nxt;
+        uint32_t ri[AP];                        // ring: first 64 entries of the next AP rows' lists
+        float rv[AP];
         auto fetch = [&](const DsMeta& m, int q, int64_t row, int slot) {
+            if (APROBE == 4) { ri[slot] = (uint32_t)lane * 29u & 2047u; rv[slot] = 0.01f * (float)lane; return; }
             const uint32_t off = __builtin_amdgcn_readlane(m.te.x, q), cnt = __builtin_amdgcn_readlane(m.te.y, q);
-            const auto di = list_rsrc(ws.ent_idx + row * ws.cap + off, cnt);
-            const auto dv = list_rsrc(ws.ent_val + row * ws.cap + off, cnt);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t e = (uint32_t)lane + 64u * h;
-                const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(di, lane * 4, h * 256, 0);
-                ri[slot][h] = e < cnt ? x : 0xFFFFFFFFu;
-                rv[slot][h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dv, lane * 4, h * 256, 0));
-            }
+            const auto de = list_rsrc(ws.ent + row * ws.cap + off, 2 * cnt);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(de, lane * 8, 0, 0);
+            ri[slot] = (uint32_t)lane < cnt ? v[0] : 0xFFFFFFFFu;       // invalid word: bits >= 20 set
+            rv[slot] = __uint_as_float(v[1]);
         };
-        auto fold = [&](uint32_t ix, float xv, float wi) {
-            const uint32_t loc = ix - cbase;
-            if (loc < (uint32_t)CHUNK) {
-                const float e = op.template apply<false>(xv, (int64_t)ix, colbase(ix), tab);
-                const float t = W ? wi * e : e;
-                if (!(t == 0.f)) {
-                    const float o = tl[loc];
-                    tl[loc] = (__float_as_uint(o) == DS_SENT) ? t : o + t;
-                }
+        auto add = [&](uint32_t loc, float t) {
+            if (APROBE != 2 && !(t == 0.f)) tl[loc] = tl[loc] + t;
+        };
+        auto row_state = [&](const DsMeta& m, int q, DsRow& rr, uint32_t& rk, uint32_t& mode, float& wi) {
+            rr.n = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.pn), q));
+            rr.rn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.rpn), q));
+            rk = __builtin_amdgcn_readlane(m.rk, q);
+            rr.rk2 = rk ^ 0x27D4EB2Fu;
+            mode = __builtin_amdgcn_readlane(m.mode, q);
+            rr.fast = (mode & DS_FAST) != 0u;
+            wi = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.w), q));
+        };
+        auto contrib = [&](uint32_t word, float xv, const DsRow& rr, float wi) {
+            float t = 0.f;
+            if (word < (1u << 20)) {
+                const float e = APROBE == 1 ? xv : ds_encode<APROBE == 3>(xv, hbase + (word & (HCHUNK - 1)), word >> 12, rr, tab, s, sf);
+                t = W ? wi * e : e;
             }
+            return t;
         };
 #pragma unroll
-        for (int q = 0; q < DS_AP; ++q) fetch(cur, q, q, q);
+        for (int q = 0; q < AP; ++q) fetch(cur, q, q, q);
         for (int64_t b = 0; b < nb; ++b) {
             const int64_t i0 = b * 64;
-            nxt = ds_meta(ws, c, n, i0 + 64 + lane, w);
-            for (int qb = 0; qb < 64; qb += DS_AP) {
+            nxt = ds_meta(ws, h, n, i0 + 64 + lane, w);
+            // rows of this batch that need the general path: dense, or more than 64 entries here
+            const uint64_t slow = __ballot((i0 + lane < n) && ((cur.mode & DS_DENSE) || cur.te.y > 64u));
+            for (int qb = 0; qb < 64; qb += AP) {
+                const int nrow = (int)min((int64_t)AP, n - (i0 + qb));
+                if (nrow == AP && ((slow >> qb) & ((AP == 64 ? 0ull : (1ull << AP)) - 1ull)) == 0ull) {
+                    // straight line: AP independent encodes (interleaved by the compiler), then
+                    // the adds in row order
+                    float t[AP];
 #pragma unroll
-                for (int u = 0; u < DS_AP; ++u) {
-                    const int q = qb + u;
-                    const int64_t row = i0 + q;
-                    if (row < n) {
-                        op.dn = make_div(__uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.pn), q)));
-                        op.rk = __builtin_amdgcn_readlane(cur.rk, q);
-                        const float wi = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.w), q));
-                        const uint32_t mode = __builtin_amdgcn_readlane(cur.mode, q);
-                        if (mode) {
-                            // dense row: every element of the chunk, coalesced
-                            const float* rp = rows.row(row) + cbase;
-                            for (int k = 0; k < CHUNK / 64; ++k) {
-                                const int e = k * 64 + lane;
-                                if (e < len) fold(cbase + (uint32_t)e, rp[e], wi);
+                    for (int u = 0; u < AP; ++u) {
+                        DsRow rr;
+                        uint32_t rk, mode;
+                        float wi;
+                        row_state(cur, qb + u, rr, rk, mode, wi);
+                        t[u] = contrib(ri[u], rv[u], rr, wi);
+                    }
+#pragma unroll
+                    for (int u = 0; u < AP; ++u)
+                        if (ri[u] < (1u << 20)) add(ri[u] & (HCHUNK - 1), t[u]);
+                } else {
+                    for (int u = 0; u < nrow; ++u) {
+                        const int q = qb + u;
+                        const int64_t row = i0 + q;
+                        DsRow rr;
+                        uint32_t rk, mode;
+                        float wi;
+                        row_state(cur, q, rr, rk, mode, wi);
+                        uint32_t rw = 0xFFFFFFFFu;
+                        float rx = 0.f;
+#pragma unroll
+                        for (int z = 0; z < AP; ++z)
+                            if (z == u) { rw = ri[z]; rx = rv[z]; }
+                        if (mode & DS_DENSE) {
+                            // dense row: every element of the half chunk, coalesced
+                            const float* rp = rows.row(row) + hbase;
+                            for (int k = 0; k < HCHUNK / 64; ++k) {
+                                const uint32_t e = (uint32_t)(k * 64 + lane);
+                                if (e < (uint32_t)len) {
+                                    const float ev = ds_encode(rp[e], hbase + e, ds_hi8(hbase + e, rk), rr, tab, s, sf);
+                                    add(e, W ? wi * ev : ev);
+                                }
                             }
                         } else {
-                            fold(ri[u][0], rv[u][0], wi);
-                            fold(ri[u][1], rv[u][1], wi);
+                            if (rw < (1u << 20)) add(rw & (HCHUNK - 1), contrib(rw, rx, rr, wi));
                             const uint32_t cnt = __builtin_amdgcn_readlane(cur.te.y, q);
-                            if (cnt > 128u) {
-                                const uint32_t off = __builtin_amdgcn_readlane(cur.te.x, q);
-                                for (uint32_t e = 128u + lane; e < cnt; e += 64)
-                                    fold(ws.ent_idx[row * ws.cap + off + e], ws.ent_val[row * ws.cap + off + e], wi);
+                            const uint32_t off = __builtin_amdgcn_readlane(cur.te.x, q);
+                            for (uint32_t e = 64u + lane; e < cnt; e += 64) {
+                                const uint2 en = ws.ent[row * ws.cap + off + e];
+                                add(en.x & (HCHUNK - 1), contrib(en.x, __uint_as_float(en.y), rr, wi));
                             }
                         }
                     }
-                    // refill the slot with row q + AP (next batch's meta past the batch end)
-                    if (q + DS_AP < 64) fetch(cur, q + DS_AP, row + DS_AP, u);
-                    else fetch(nxt, q + DS_AP - 64, row + DS_AP, u);
+                }
+                // refill the slots with rows qb + AP .. (next batch's meta past the batch end)
+#pragma unroll
+                for (int u = 0; u < AP; ++u) {
+                    const int q = qb + u;
+                    if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, u);
+                    else fetch(nxt, q + AP - 64, i0 + q + AP, u);
                 }
             }
             cur = nxt;
         }
         // untouched columns: every contribution was +-0; the sequential fold gives -0 only if all
         // are -0.  Sign of row i's zero: C(x) = copysign(0, x) * norm (+0 for x == 0), times w_i.
-        for (int k = 0; k < CHUNK / 64; ++k) {
+        for (int k = 0; k < HCHUNK / 64; ++k) {
             const int e = k * 64 + lane;
-            bool neg = e < len && __float_as_uint(tl[e]) == DS_SENT;
+            bool neg = e < len && __float_as_uint(tl[e]) == 0x80000000u;
             if (__ballot(neg) == 0ull) continue;
             const bool mine = neg;
             for (int64_t i = 0; i < n && __ballot(neg) != 0ull; ++i) {
                 if (neg) {
-                    const float xv = rows.row(i)[cbase + e];
+                    const float xv = rows.row(i)[hbase + e];
                     const bool zs = (xv != 0.f) && (__float_as_uint(xv) >> 31);
                     const bool ws_ = W && (__float_as_uint(w[i]) >> 31);
                     neg = zs != ws_;
@@ -425,35 +539,40 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
             }
             if (mine) tl[e] = neg ? -0.f : 0.f;
         }
-        for (int64_t i = lane; i < len; i += 64) out[cbase + i] = tl[i] / wt;
+        for (int64_t i = lane; i < len; i += 64) out[hbase + i] = tl[i] / wt;
     }
 }
 
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
-static int64_t ds_cap(int s, int64_t d) {
-    // 2x the s sqrt(D) bound on the expected nonzeros (n_lo >= n / 2), the hi8 slack and margin
-    const double b = 2.0 * (double)s * sqrt((double)d) + (double)d / 256.0 + 2.0 * DS_FGS * CHUNK;
-    int64_t cap = std::min<int64_t>(d, (int64_t)b);
-    return std::max<int64_t>((cap + 3) & ~int64_t(3), 4);
+// Filter variant (tuning runs: FLC_DS_GCAP=1024 doubles the per-item staging and list regions,
+// FLC_DS_GRID=res launches a resident-only grid instead of the oversubscribed one).
+struct DsVariant { int gcap; bool resident; int ap; };
+static DsVariant ds_variant() {
+    DsVariant v{DS_GCAP, false, DS_AP};
+    if (const char* e = getenv("FLC_DS_AP")) v.ap = atoi(e);
+    if (const char* e = getenv("FLC_DS_GCAP")) v.gcap = atoi(e) == 1024 ? 1024 : DS_GCAP;
+    if (const char* e = getenv("FLC_DS_GRID")) v.resident = !strcmp(e, "res");
+    return v;
 }
 
-static DsWs carve_ds(void* base, int s, int64_t n, int64_t d, size_t* bytes) {
+static DsWs carve_ds(void* base, int64_t n, int64_t d, int gcap, size_t* bytes) {
     Carver cv(base);
-    const int64_t C = std::max<int64_t>(nchunks(d), 1), nn = std::max<int64_t>(n, 1);
+    const int64_t C = std::max<int64_t>(nchunks(d), 1), H = std::max<int64_t>(nhalves(d), 1);
+    const int64_t nn = std::max<int64_t>(n, 1);
     DsWs w;
-    w.cap = ds_cap(s, d);
     w.G = (C + DS_FGS - 1) / DS_FGS;
-    w.tab = cv.take<uint2>((size_t)C * nn);
-    w.ent_idx = cv.take<uint32_t>((size_t)nn * w.cap);
-    w.ent_val = cv.take<float>((size_t)nn * w.cap);
-    w.rowcnt = cv.take<uint32_t>((size_t)nn * RCS);
+    w.cap = w.G * gcap;
+    w.tab = cv.take<uint2>((size_t)std::max<int64_t>(H, w.G * 2 * DS_FGS) * nn);   // + padding halves
+    w.ent = cv.take<uint2>((size_t)nn * w.cap);
+    w.ovfi = cv.take<uint32_t>((size_t)nn * w.G);
     w.flags = cv.take<uint32_t>(nn);
     w.qc = cv.take<float>(nn);
     w.nlo = cv.take<float>(nn);
     w.partial = cv.take<double>((size_t)nn * w.G);
     w.pn = cv.take<float>(nn);
+    w.rpn = cv.take<float>(nn);
     w.rk = cv.take<uint32_t>(nn);
     if (bytes) *bytes = cv.bytes();
     return w;
@@ -482,36 +601,68 @@ bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n,
 }
 
 size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
+    (void)prm;
     size_t b = 0;
-    carve_ds(nullptr, prm->s, n, d, &b);
+    carve_ds(nullptr, n, d, ds_variant().gcap, &b);
     return b;
 }
 
 int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d, const float* w,
            float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
+    const DsVariant v = ds_variant();
     size_t need = 0;
-    carve_ds(nullptr, prm->s, n, d, &need);
+    carve_ds(nullptr, n, d, v.gcap, &need);
     if (ws_bytes < need) { set_error("dithering (sparse): workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
-    DsWs ws = carve_ds(wsp, prm->s, n, d, nullptr);
+    DsWs ws = carve_ds(wsp, n, d, v.gcap, nullptr);
     const int64_t client0 = pat ? pat->client0 : 0;
-    const int64_t C = nchunks(d);
+    const int64_t H = nhalves(d);
     { ProfScope _ps("k_ds_sample", st);
     hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->seed, client0, ws); }
     FLC_CHECK_LAUNCH("k_ds_sample");
     {
-        const int64_t waves = n * ws.G;
-        const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 32768));
-        ProfScope _ps("k_ds_filter", st);
-        hipLaunchKernelGGL((k_ds_filter<16>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+        auto launch = [&](auto kern) {
+            const int64_t waves = n * ws.G;
+            int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 32768));
+            if (v.resident) {
+                int per = 0, dev = 0, cus = 0;
+                if (hipGetDevice(&dev) == hipSuccess &&
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) == hipSuccess && per > 0)
+                    gw = std::min(gw, per * cus);
+            }
+            ProfScope _ps("k_ds_filter", st);
+            hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+        };
+        const char* pe = getenv("FLC_DS_PROBE");
+        const int probe = pe ? atoi(pe) : 0;
+        if (probe == 1) launch(k_ds_filter<16, DS_GCAP, 1>);
+        else if (probe == 2) launch(k_ds_filter<16, DS_GCAP, 2>);
+        else if (probe == 3) launch(k_ds_filter<16, DS_GCAP, 3>);
+        else if (probe == 4) launch(k_ds_filter<16, DS_GCAP, 4>);
+        else if (probe == 5) launch(k_ds_filter<16, DS_GCAP, 5>);
+        else if (probe == 6) launch(k_ds_filter<16, DS_GCAP, 6>);
+        else if (v.gcap == 1024) launch(k_ds_filter<16, 1024>);
+        else launch(k_ds_filter<16, DS_GCAP>);
     }
     FLC_CHECK_LAUNCH("k_ds_filter");
     hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, n, ws, w, pnorm_out);
     FLC_CHECK_LAUNCH("k_ds_final");
     {
-        const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((C + 3) / 4, 4096));
+        const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + 3) / 4, 8192));
         ProfScope _ps("k_ds_accum", st);
-        if (w) hipLaunchKernelGGL((k_ds_accum<true>), dim3(ab), dim3(256), 0, st, rows, n, d, ws, prm->d_levels, prm->s, w, wt, out);
-        else hipLaunchKernelGGL((k_ds_accum<false>), dim3(ab), dim3(256), 0, st, rows, n, d, ws, prm->d_levels, prm->s, w, wt, out);
+        auto go = [&](auto kw, auto kn) {
+            if (w) hipLaunchKernelGGL(kw, dim3(ab), dim3(256), 0, st, rows, n, d, ws, prm->d_levels, prm->s, w, wt, out);
+            else hipLaunchKernelGGL(kn, dim3(ab), dim3(256), 0, st, rows, n, d, ws, prm->d_levels, prm->s, w, wt, out);
+        };
+        const char* ape = getenv("FLC_DS_APROBE");
+        const int aprobe = ape ? atoi(ape) : 0;
+        if (aprobe == 1) go(k_ds_accum<true, DS_AP, 1>, k_ds_accum<false, DS_AP, 1>);
+        else if (aprobe == 2) go(k_ds_accum<true, DS_AP, 2>, k_ds_accum<false, DS_AP, 2>);
+        else if (aprobe == 3) go(k_ds_accum<true, DS_AP, 3>, k_ds_accum<false, DS_AP, 3>);
+        else if (aprobe == 4) go(k_ds_accum<true, DS_AP, 4>, k_ds_accum<false, DS_AP, 4>);
+        else if (v.ap == 16) go(k_ds_accum<true, 16>, k_ds_accum<false, 16>);
+        else if (v.ap == 32) go(k_ds_accum<true, 32>, k_ds_accum<false, 32>);
+        else go(k_ds_accum<true, DS_AP>, k_ds_accum<false, DS_AP>);
     }
     FLC_CHECK_LAUNCH("k_ds_accum");
     return FLC_OK;

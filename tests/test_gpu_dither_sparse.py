@@ -76,10 +76,12 @@ def make_rows(kind, n, d, g):
         return r
     if kind == "ones":       # flat rows: the s sqrt(D) bound is attained
         return np.sign(g.standard_normal((n, d))).astype(np.float32)
+    if kind == "tiny":       # norms near FLT_MIN: levels * norm are subnormal (fold must keep them)
+        return (g.standard_normal((n, d)) * 1e-41).astype(np.float32)
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["normal", "heavy", "sparse", "negative", "clustered", "ones"])
+@pytest.mark.parametrize("kind", ["normal", "heavy", "sparse", "negative", "clustered", "ones", "tiny"])
 @pytest.mark.parametrize("spec", ["qsgd:4", "qsgd:127"])
 def test_sparse_dither_vs_oracle(ag, monkeypatch, kind, spec):
     monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
