@@ -18,8 +18,8 @@ Workloads (BASELINE.json configs; the default is the largest single-GPU config, 
 Algorithmic bytes: topk / qsgd / ident 4*N*D + 4*D; randk 4*N*K + 4*D (device-RNG
 indices cost no bytes).  value = algorithmic bytes of all ranks / max-over-ranks step time.
 
-roofline: the dominant kernel's algorithmic bytes per launch / its mean launch time, timed with
-HIP events on its launch stream inside the timed region (flc_profile_*); peak 8.0 TB/s
+roofline: the dominant kernel's algorithmic bytes per step / its summed launch time per step, timed
+with HIP events on its launch stream inside the timed region (flc_profile_*); peak 8.0 TB/s
 (MI355X_MICROARCH.md).  traffic: HBM bytes per launch from rocprofv3 PMC passes
 (profiles/pmc_<workload>.json, written by profiles/collect_pmc.py), or null.
 cpu_baseline: the oracle (numpy restatement of the reference path) timed on this host, rank 0.
@@ -242,9 +242,12 @@ def main():
     step_ms = elapsed / args.steps * 1e3
     total_bytes = algorithmic_bytes(spec, n, d, k) * world
     value = total_bytes / (elapsed / args.steps) / 1e9
+    # the dominant kernel may run as several launches per step (sparse QSGD: one per row group):
+    # its achieved rate is the algorithmic bytes of a step over its summed launch time per step
     kb = kernel_bytes(wl["kernel"], n, d, k)
     kavg_ms = kms / max(klaunch, 1)
-    achieved = kb / (kavg_ms * 1e-3) / 1e9 if klaunch else None
+    kstep_ms = kms / args.steps
+    achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
@@ -273,7 +276,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": wl["kernel"],
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBS, 4) if achieved else None, "traffic": traffic,
-                         "bytes_per_launch": kb, "avg_launch_ms": round(kavg_ms, 4), "launches": klaunch,
+                         "bytes_per_step": kb, "kernel_ms_per_step": round(kstep_ms, 4),
+                         "avg_launch_ms": round(kavg_ms, 4), "launches": klaunch,
                          "other_kernels_avg_ms": others},
             "cpu_baseline": cpu,
         }

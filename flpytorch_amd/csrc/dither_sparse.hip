@@ -32,6 +32,10 @@
 // has h >= p 2^32, so hi8 = h >> 24 > 256 p - 1 >= 255 - 256 |x| (1 + 2^-24) / (l1 n_lo) - 2^-15,
 // and  |x| qc + hi8 > 255 - 2^-15;  the fp32 fma loses < 2^-14 there, so  > 254.98  keeps every
 // nonzero.  Elements in higher intervals (y >= l1) have |x| qc >= 256.
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "chunks.hpp"
 #include "codec_ops.hpp"
 
@@ -56,6 +60,7 @@ struct DsWs {
     float* pn;            // [N] norm
     float* rpn;           // [N] RN(1 / norm)
     uint32_t* rk;         // [N] device-RNG row key
+    float* part;          // [D] running sums carried between the row groups' folds
     int64_t cap;          // per row: G * GCAP (each filter item owns a fixed region)
     int64_t G;            // filter items per row
 };
@@ -144,7 +149,7 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // 5 copy-out into one fixed per-wave scratch region (L2-resident: stores without HBM traffic);
 // 6 full with non-temporal copy-out stores
 template <int RING, int GCAP, int PROBE = 0>
-__global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64_t d, DsWs ws) {
+__global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, DsWs ws) {
     constexpr int FGS = DS_FGS;
     constexpr int NH = 2 * FGS;                               // half chunks per item
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
@@ -153,17 +158,16 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
     __shared__ uint2 stage[4][GCAP];                         // (entry word, x bits)
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t H = nhalves(d);
     const int64_t G = ws.G;
-    const int64_t items = n * G;
+    const int64_t items = rn * G;                            // this launch's rows: [r0, r0 + rn)
     const int64_t stride = (int64_t)gridDim.x * 4;
     int64_t it = (int64_t)blockIdx.x * 4 + wv;
     if (it >= items) return;
     const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
     uint2* sg = stage[wv];
     float4 ring[RING];
-    int64_t row = it / G;
-    int64_t c = (it - row * G) * FGS;
+    int64_t row = r0 + it / G;
+    int64_t c = (it - (row - r0) * G) * FGS;
     auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
 #pragma unroll
     for (int L = 0; L < RING - 1; ++L) {
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
     while (it < items) {
         const float qc = sload(ws.qc + row);
         const uint32_t rk = sload(ws.rk + row);
-        const int64_t gi = it - row * G;
+        const int64_t gi = it - (row - r0) * G;
         const int64_t nit = it + stride;
         uint32_t cnt = 0;
         uint32_t hc[NH];                                      // running count at each half's end
@@ -194,8 +198,8 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
             if (sub + 1 < FGS) {
                 rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
             } else if (nit < items) {
-                nrow = nit / G;
-                nc = (nit - nrow * G) * FGS;
+                nrow = r0 + nit / G;
+                nc = (nit - (nrow - r0) * G) * FGS;
                 rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
             } else {
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
@@ -288,11 +292,11 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
 // ------------------------------------------------------------------------------------------
 // Norm and row mode: one wave per row.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ds_final(int64_t n, DsWs ws, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void k_ds_final(int64_t r0, int64_t rn, DsWs ws, const float* __restrict__ w,
                                                   float* __restrict__ pnorm_out) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= n) return;
+    const int64_t row = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= r0 + rn) return;
     double a = 0.0;
     uint32_t ov = 0;
     for (int64_t k = lane; k < ws.G; k += 64) { a += ws.partial[row * ws.G + k]; ov |= ws.ovfi[row * ws.G + k]; }
@@ -324,11 +328,11 @@ struct DsMeta {
     uint32_t rk, mode;
 };
 
-__device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r, const float* w) {
+__device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t rend, int64_t r, const float* w) {
     DsMeta m;
     m.te = make_uint2(0, 0);
     m.pn = 1.f; m.rpn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
-    if (r < n) {
+    if (r < rend) {
         m.te = ws.tab[c * n + r];           // c: half-chunk index
         m.pn = ws.pn[r];
         m.rpn = ws.rpn[r];
@@ -398,11 +402,15 @@ __device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow
 __device__ inline uint32_t ds_hi8(uint32_t j, uint32_t rk) { return (grouphash(j >> 2, rk) >> (8u * (j & 3u))) & 0xFFu; }
 
 // APROBE (tuning runs only, FLC_DS_APROBE; outputs invalid): 1 no encode (t = x); 2 no tile adds;
-// 3 encode without the level-table lookup; 4 no list fetch (constant in-range entries)
+// 3 encode without the level-table lookup; 4 no list fetch (constant in-range entries); 7 = 1+2+4
+// Folds rows [r0, r0 + rn) into the running sums: the first group starts the tiles at -0, the others
+// continue from `part` (the previous group's tiles); the last group resolves untouched columns
+// over ALL n rows and writes out = sums / wt, the others write their tiles back to `part`.
 template <bool W, int AP, int APROBE = 0>
-__global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_t d, DsWs ws,
-                                                  const float* __restrict__ levels, int s,
-                                                  const float* __restrict__ w, float wt, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
+                                                  int64_t d, DsWs ws, const float* __restrict__ levels, int s,
+                                                  const float* __restrict__ w, float wt, float* __restrict__ part,
+                                                  float* __restrict__ out) {
     static_assert(64 % AP == 0, "row groups tile the 64-row batch");
     __shared__ __attribute__((aligned(16))) float tile[4][HCHUNK];
     __shared__ __attribute__((aligned(16))) float4 tab[DS_MAXS];
@@ -411,7 +419,8 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t H = nhalves(d);
     float* tl = tile[wv];
-    const int64_t nb = (n + 63) / 64;
+    const int64_t rend = r0 + rn;
+    const int64_t nb = (rn + 63) / 64;
     const float sf = (float)s;
     for (int64_t h = (int64_t)blockIdx.x * 4 + wv; h < H; h += (int64_t)gridDim.x * 4) {
         // The tile starts at -0.0: (-0) + t == t for every nonzero t, and a column that received a
@@ -420,14 +429,14 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
         // Adds are read-modify-writes of the wave's own tile, in row order (one wave executes its
         // LDS operations in program order; the lanes of one instruction hit distinct columns), so
         // each column sees its rows' terms in row order.  (ds_add_f32 atomics measured 30 % slower.)
-        for (int i = lane; i < HCHUNK; i += 64) tl[i] = -0.f;
         const uint32_t hbase = (uint32_t)(h * HCHUNK);
         const int64_t len = min((int64_t)HCHUNK, d - (int64_t)hbase);
-        DsMeta cur = ds_meta(ws, h, n, lane, w), nxt;
+        for (int i = lane; i < HCHUNK; i += 64) tl[i] = (first || i >= len) ? -0.f : part[hbase + i];
+        DsMeta cur = ds_meta(ws, h, n, rend, r0 + lane, w), nxt;
         uint32_t ri[AP];                        // ring: first 64 entries of the next AP rows' lists
         float rv[AP];
         auto fetch = [&](const DsMeta& m, int q, int64_t row, int slot) {
-            if (APROBE == 4) { ri[slot] = (uint32_t)lane * 29u & 2047u; rv[slot] = 0.01f * (float)lane; return; }
+            if (APROBE == 4 || APROBE == 7) { ri[slot] = (uint32_t)lane * 29u & 2047u; rv[slot] = 0.01f * (float)lane; return; }
             const uint32_t off = __builtin_amdgcn_readlane(m.te.x, q), cnt = __builtin_amdgcn_readlane(m.te.y, q);
             const auto de = list_rsrc(ws.ent + row * ws.cap + off, 2 * cnt);
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(de, lane * 8, 0, 0);
@@ -435,7 +444,7 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
             rv[slot] = __uint_as_float(v[1]);
         };
         auto add = [&](uint32_t loc, float t) {
-            if (APROBE != 2 && !(t == 0.f)) tl[loc] = tl[loc] + t;
+            if (APROBE != 2 && APROBE != 7 && !(t == 0.f)) tl[loc] = tl[loc] + t;
         };
         auto row_state = [&](const DsMeta& m, int q, DsRow& rr, uint32_t& rk, uint32_t& mode, float& wi) {
             rr.n = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.pn), q));
@@ -449,20 +458,20 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
         auto contrib = [&](uint32_t word, float xv, const DsRow& rr, float wi) {
             float t = 0.f;
             if (word < (1u << 20)) {
-                const float e = APROBE == 1 ? xv : ds_encode<APROBE == 3>(xv, hbase + (word & (HCHUNK - 1)), word >> 12, rr, tab, s, sf);
+                const float e = (APROBE == 1 || APROBE == 7) ? xv : ds_encode<APROBE == 3>(xv, hbase + (word & (HCHUNK - 1)), word >> 12, rr, tab, s, sf);
                 t = W ? wi * e : e;
             }
             return t;
         };
 #pragma unroll
-        for (int q = 0; q < AP; ++q) fetch(cur, q, q, q);
+        for (int q = 0; q < AP; ++q) fetch(cur, q, r0 + q, q);
         for (int64_t b = 0; b < nb; ++b) {
-            const int64_t i0 = b * 64;
-            nxt = ds_meta(ws, h, n, i0 + 64 + lane, w);
+            const int64_t i0 = r0 + b * 64;
+            nxt = ds_meta(ws, h, n, rend, i0 + 64 + lane, w);
             // rows of this batch that need the general path: dense, or more than 64 entries here
-            const uint64_t slow = __ballot((i0 + lane < n) && ((cur.mode & DS_DENSE) || cur.te.y > 64u));
+            const uint64_t slow = __ballot((i0 + lane < rend) && ((cur.mode & DS_DENSE) || cur.te.y > 64u));
             for (int qb = 0; qb < 64; qb += AP) {
-                const int nrow = (int)min((int64_t)AP, n - (i0 + qb));
+                const int nrow = (int)min((int64_t)AP, rend - (i0 + qb));
                 if (nrow == AP && ((slow >> qb) & ((AP == 64 ? 0ull : (1ull << AP)) - 1ull)) == 0ull) {
                     // straight line: AP independent encodes (interleaved by the compiler), then
                     // the adds in row order
@@ -522,6 +531,10 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
             }
             cur = nxt;
         }
+        if (!last) {
+            for (int64_t i = lane; i < len; i += 64) part[hbase + i] = tl[i];
+            continue;
+        }
         // untouched columns: every contribution was +-0; the sequential fold gives -0 only if all
         // are -0.  Sign of row i's zero: C(x) = copysign(0, x) * norm (+0 for x == 0), times w_i.
         for (int k = 0; k < HCHUNK / 64; ++k) {
@@ -574,6 +587,7 @@ static DsWs carve_ds(void* base, int64_t n, int64_t d, int gcap, size_t* bytes) 
     w.pn = cv.take<float>(nn);
     w.rpn = cv.take<float>(nn);
     w.rk = cv.take<uint32_t>(nn);
+    w.part = cv.take<float>((size_t)std::max<int64_t>(d, 1));
     if (bytes) *bytes = cv.bytes();
     return w;
 }
@@ -607,6 +621,22 @@ size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     return b;
 }
 
+// Per-device side stream and events of the row-group pipeline (lazily created, mutex-guarded;
+// enqueueing under the mutex keeps concurrent callers' event records and waits paired).
+namespace {
+struct DsCtx {
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev;
+};
+std::mutex g_ds_mu;
+std::map<int, DsCtx> g_ds_ctx;
+}  // namespace
+
+static int ds_groups(int64_t n) {
+    if (const char* e = getenv("FLC_DS_GROUPS")) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), n));
+    return 1;   // measured: folds beside filters are starved (K = 2..8 no faster than 1)
+}
+
 int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d, const float* w,
            float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
     const DsVariant v = ds_variant();
@@ -616,13 +646,15 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     DsWs ws = carve_ds(wsp, n, d, v.gcap, nullptr);
     const int64_t client0 = pat ? pat->client0 : 0;
     const int64_t H = nhalves(d);
-    { ProfScope _ps("k_ds_sample", st);
-    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->seed, client0, ws); }
-    FLC_CHECK_LAUNCH("k_ds_sample");
-    {
+    const char* pe = getenv("FLC_DS_PROBE");
+    const int probe = pe ? atoi(pe) : 0;
+    const char* ape = getenv("FLC_DS_APROBE");
+    const int aprobe = ape ? atoi(ape) : 0;
+    const int K = ds_groups(n);
+
+    auto filter = [&](int64_t r0, int64_t rn) -> int {
         auto launch = [&](auto kern) {
-            const int64_t waves = n * ws.G;
-            int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 32768));
+            int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
             if (v.resident) {
                 int per = 0, dev = 0, cus = 0;
                 if (hipGetDevice(&dev) == hipSuccess &&
@@ -631,40 +663,73 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
                     gw = std::min(gw, per * cus);
             }
             ProfScope _ps("k_ds_filter", st);
-            hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+            hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, d, ws);
         };
-        const char* pe = getenv("FLC_DS_PROBE");
-        const int probe = pe ? atoi(pe) : 0;
-        if (probe == 1) launch(k_ds_filter<16, DS_GCAP, 1>);
-        else if (probe == 2) launch(k_ds_filter<16, DS_GCAP, 2>);
+        if (probe == 2) launch(k_ds_filter<16, DS_GCAP, 2>);
         else if (probe == 3) launch(k_ds_filter<16, DS_GCAP, 3>);
         else if (probe == 4) launch(k_ds_filter<16, DS_GCAP, 4>);
-        else if (probe == 5) launch(k_ds_filter<16, DS_GCAP, 5>);
-        else if (probe == 6) launch(k_ds_filter<16, DS_GCAP, 6>);
         else if (v.gcap == 1024) launch(k_ds_filter<16, 1024>);
         else launch(k_ds_filter<16, DS_GCAP>);
-    }
-    FLC_CHECK_LAUNCH("k_ds_filter");
-    hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, n, ws, w, pnorm_out);
-    FLC_CHECK_LAUNCH("k_ds_final");
-    {
+        FLC_CHECK_LAUNCH("k_ds_filter");
+        hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((rn + 3) / 4)), dim3(256), 0, st, r0, rn, ws, w, pnorm_out);
+        FLC_CHECK_LAUNCH("k_ds_final");
+        return FLC_OK;
+    };
+    auto accum = [&](int64_t r0, int64_t rn, int first, int last, hipStream_t s2) -> int {
         const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + 3) / 4, 8192));
-        ProfScope _ps("k_ds_accum", st);
+        ProfScope _ps("k_ds_accum", s2);
         auto go = [&](auto kw, auto kn) {
-            if (w) hipLaunchKernelGGL(kw, dim3(ab), dim3(256), 0, st, rows, n, d, ws, prm->d_levels, prm->s, w, wt, out);
-            else hipLaunchKernelGGL(kn, dim3(ab), dim3(256), 0, st, rows, n, d, ws, prm->d_levels, prm->s, w, wt, out);
+            if (w) hipLaunchKernelGGL(kw, dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels,
+                                      prm->s, w, wt, ws.part, out);
+            else hipLaunchKernelGGL(kn, dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels,
+                                    prm->s, w, wt, ws.part, out);
         };
-        const char* ape = getenv("FLC_DS_APROBE");
-        const int aprobe = ape ? atoi(ape) : 0;
         if (aprobe == 1) go(k_ds_accum<true, DS_AP, 1>, k_ds_accum<false, DS_AP, 1>);
         else if (aprobe == 2) go(k_ds_accum<true, DS_AP, 2>, k_ds_accum<false, DS_AP, 2>);
-        else if (aprobe == 3) go(k_ds_accum<true, DS_AP, 3>, k_ds_accum<false, DS_AP, 3>);
         else if (aprobe == 4) go(k_ds_accum<true, DS_AP, 4>, k_ds_accum<false, DS_AP, 4>);
-        else if (v.ap == 16) go(k_ds_accum<true, 16>, k_ds_accum<false, 16>);
-        else if (v.ap == 32) go(k_ds_accum<true, 32>, k_ds_accum<false, 32>);
+        else if (aprobe == 7) go(k_ds_accum<true, DS_AP, 7>, k_ds_accum<false, DS_AP, 7>);
         else go(k_ds_accum<true, DS_AP>, k_ds_accum<false, DS_AP>);
+        FLC_CHECK_LAUNCH("k_ds_accum");
+        return FLC_OK;
+    };
+
+    { ProfScope _ps("k_ds_sample", st);
+    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->seed, client0, ws); }
+    FLC_CHECK_LAUNCH("k_ds_sample");
+    if (K == 1) {
+        int rc = filter(0, n);
+        if (rc) return rc;
+        return accum(0, n, 1, 1, st);
     }
-    FLC_CHECK_LAUNCH("k_ds_accum");
+    // Row-group pipeline: the fold of group g (side stream, latency-bound) runs under the filter
+    // of group g + 1 (caller stream, HBM-bound); the groups' folds continue one another's tiles
+    // through `part`, in row order.
+    int dev = 0;
+    FLC_CHECK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_ds_mu);
+    DsCtx& cx = g_ds_ctx[dev];
+    if (!cx.side) {
+        // the fold is latency-bound and short: it gets the dispatcher's priority over the filter
+        int lo = 0, hi = 0;
+        FLC_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        FLC_CHECK_HIP(hipStreamCreateWithPriority(&cx.side, hipStreamNonBlocking, hi));
+    }
+    while ((int)cx.ev.size() < K + 1) {
+        hipEvent_t e;
+        FLC_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        cx.ev.push_back(e);
+    }
+    for (int g = 0; g < K; ++g) {
+        const int64_t r0 = n * g / K, r1 = n * (g + 1) / K;
+        int rc = filter(r0, r1 - r0);
+        if (rc) return rc;
+        FLC_CHECK_HIP(hipEventRecord(cx.ev[g], st));
+        FLC_CHECK_HIP(hipStreamWaitEvent(cx.side, cx.ev[g], 0));
+        rc = accum(r0, r1 - r0, g == 0, g == K - 1, cx.side);
+        if (rc) return rc;
+    }
+    FLC_CHECK_HIP(hipEventRecord(cx.ev[K], cx.side));
+    FLC_CHECK_HIP(hipStreamWaitEvent(st, cx.ev[K], 0));
     return FLC_OK;
 }
 

@@ -128,6 +128,28 @@ def test_sparse_dither_weights_nonfinite(ag, monkeypatch, bad):
     assert_bitexact(red(torch.from_numpy(rows).cuda(), client0=client0, weights=w), want)
 
 
+@pytest.mark.parametrize("groups", [2, 3])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_sparse_dither_row_groups(ag, monkeypatch, groups, weighted):
+    """The row-group pipeline (filter of group g+1 beside the fold of group g on a side stream; the
+    folds continue each other's sums) gives the same bits as the sequential fold."""
+    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
+    monkeypatch.setenv("FLC_DS_GROUPS", str(groups))
+    n, d, client0 = 7, 150_001, 3
+    g = np.random.default_rng(groups)
+    rows = make_rows("normal", n, d, g)
+    rows[2] = make_rows("negative", 1, d, g)[0]
+    rows[5] = make_rows("clustered", 1, d, g)[0]          # a dense-folded row inside a group
+    w = [1.0, -0.5, 2.0, 1.5, 0.25, 1.0, 3.0] if weighted else None
+    want, wn = oracle_uplink("qsgd:16", rows, client0, weights=w)
+    red = ag.UplinkReducer(ag.initCompressor("qsgd:16", d), seed=SEED)
+    pn = torch.empty(n, device="cuda")
+    got = red(torch.from_numpy(rows).cuda(), client0=client0, weights=w, pnorms_out=pn)
+    torch.cuda.synchronize()
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)
+
+
 def test_sparse_equals_dense_c4_scale(ag, monkeypatch):
     """C4's row length (D = 25 M, qsgd:127): the sparse path and the dense two-pass path give
     the same bits, and the same norms (the oracle would take minutes at this size)."""
