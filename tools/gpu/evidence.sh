@@ -15,4 +15,6 @@ for wl in c3 c4; do
      python bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline > $out/stats_$wl.log 2>&1 || exit $?
 done
 timeout -k 10 300 python tools/collect_pmc.py --workload c3 > $out/pmc_c3.log 2>&1 || exit $?
+timeout -k 10 300 python tools/collect_pmc.py --workload c4 > $out/pmc_c4.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --workload c4 > $out/bench_c4.log 2>&1 || exit $?
 exit 0
