@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libflcodec%s.so" % (
     ("_" + os.environ["FLC_LIB_VARIANT"]) if os.environ.get("FLC_LIB_VARIANT") else ""))
 
 FLC_OK, FLC_ERR_ARG, FLC_ERR_DTYPE, FLC_ERR_HIP, FLC_ERR_WORKSPACE, FLC_ERR_UNSUPPORTED = range(6)
-FLC_IDENT, FLC_LAZY, FLC_RANDK, FLC_NATURAL, FLC_STD_DITHERING, FLC_NAT_DITHERING, FLC_TOPK = range(1, 8)
+FLC_IDENT, FLC_LAZY, FLC_RANDK, FLC_NATURAL, FLC_STD_DITHERING, FLC_NAT_DITHERING, FLC_TOPK, FLC_RANK_K = range(1, 9)
 FLC_NORM_LINF, FLC_NORM_L1, FLC_NORM_L2 = 0, 1, 2
 FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
 

@@ -261,7 +261,7 @@ class Compressor:
         t = self.compressorType
         prm = _lib.FlcCodecParams()
         prm.codec = int(t)
-        if t in (CompressorType.RANDK_COMPRESSOR, CompressorType.TOPK_COMPRESSOR):
+        if t in (CompressorType.RANDK_COMPRESSOR, CompressorType.TOPK_COMPRESSOR, CompressorType.RANK_K_COMPRESSOR):
             prm.k = int(self.K)
         if t == CompressorType.RANDK_COMPRESSOR:
             prm.randk_scale = float(np.float32(self.D / self.K))
@@ -291,7 +291,9 @@ class Compressor:
             out = x                                                     # alias, like the reference
             self.last_need_to_send_advance = d
         elif t == CompressorType.RANK_K_COMPRESSOR:
-            raise NotImplementedError("rank_k (dense SVD, SURVEY §8f) is not in flcodec yet")
+            out = self._encode_gpu(x)
+            # only the dyadic expansion is sent: K' (A + B), K' = min(K, min(A, B)) (compressors.py:348, 362)
+            self.last_need_to_send_advance = min(self.K, self.A, self.B) * (self.A + self.B)
         else:
             out = self._encode_gpu(x)
             if t == CompressorType.LAZY_COMPRESSOR:

@@ -30,8 +30,6 @@ class UplinkReducer:
         self.comp = compressor
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.seed = seed
-        if compressor.compressorType == CompressorType.RANK_K_COMPRESSOR:
-            raise NotImplementedError("rank_k is not in flcodec yet (SURVEY §8f)")
 
     def params(self):
         prm, keep = self.comp.codec_params(self.device)

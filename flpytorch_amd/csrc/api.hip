@@ -58,7 +58,7 @@ void prof_record(const char* name, hipStream_t st, bool begin) {
 }
 
 static bool is_sel(int codec) { return codec == FLC_TOPK || codec == FLC_RANDK; }
-static bool known(int codec) { return codec >= FLC_IDENT && codec <= FLC_TOPK; }
+static bool known(int codec) { return codec >= FLC_IDENT && codec <= FLC_RANK_K; }
 
 }  // namespace flc
 
@@ -111,6 +111,7 @@ extern "C" int flc_selftest_division(const float* d_divisors, int n, unsigned lo
 extern "C" size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t d) {
     if (!prm || !known(prm->codec)) return 0;
     if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
+    if (prm->codec == FLC_RANK_K) return rk_workspace(prm, 1, d, false);
     if (prm->codec == FLC_RANDK) return 0;
     return ew_workspace(prm, 1, d);
 }
@@ -118,6 +119,7 @@ extern "C" size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t
 extern "C" size_t flc_encode_reduce_workspace_size(const flc_codec_params* prm, int64_t n, int64_t d) {
     if (!prm || !known(prm->codec)) return 0;
     if (is_sel(prm->codec)) return sel_workspace(prm, n, d);
+    if (prm->codec == FLC_RANK_K) return rk_workspace(prm, n, d, true);
     return ew_workspace(prm, n, d);
 }
 
@@ -132,6 +134,10 @@ extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, c
         case FLC_RANDK:
             if (!(pat && pat->d_randk_idx) && prm->k > d) { set_error("randk: K > D"); return FLC_ERR_ARG; }
             return randk_dense(prm, pat, d_x, d, d_out, st);
+        case FLC_RANK_K: {
+            RowSrc r{d_x, d, nullptr};
+            return rk_run(prm, r, 1, d, /*reduce=*/false, nullptr, 1.f, d_out, d_ws, ws_bytes, st);
+        }
         case FLC_TOPK: {
             RowSrc r{d_x, d, nullptr};
             return sel_run(prm, pat, r, vec, 1, d, /*assign=*/true, nullptr, 1.f, d_out, d_ws, ws_bytes, st);
@@ -162,6 +168,10 @@ extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern*
     if (prm->codec == FLC_IDENT) {
         RowSrc s{d_rows, ld, d_row_ptrs};
         return reduce_impl(s, vec, n, d, nullptr, d_w, w_total, FLC_REDUCE_PLAIN, d_out, st);
+    }
+    if (prm->codec == FLC_RANK_K) {
+        RowSrc r{d_rows, ld, d_row_ptrs};
+        return rk_run(prm, r, n, d, /*reduce=*/true, d_w, w_total, d_out, d_ws, ws_bytes, st);
     }
     if (is_sel(prm->codec)) {
         RowSrc r{d_rows, ld, d_row_ptrs};

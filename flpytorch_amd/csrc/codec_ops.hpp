@@ -68,7 +68,14 @@ __device__ inline bool draw_below(const double* urow, uint32_t rk, int64_t j, ui
     if (COMPAT) return urow[j] < (double)p;
     uint32_t t;
     asm("v_cvt_u32_f32 %0, %1" : "=v"(t) : "v"(ceilf(p2)));   // saturating: thr32(p)
-    return dev_draw(cs, hg, (uint32_t)j, rk) < t;
+    // the draw's top byte decides unless it equals t's (1 in 256): only those lanes hash the low part
+    const uint32_t hi8 = (hg >> (8u * ((uint32_t)j & 3u))) & 0xFFu, th = t >> 24;
+    bool below = hi8 < th;
+    const bool tie = hi8 == th;
+    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
+        if (tie) below = dev_draw(cs, hg, (uint32_t)j, rk) < t;
+    }
+    return below;
 }
 template <bool COMPAT>
 __device__ inline uint32_t hg_of(uint32_t rk, int64_t j) { return COMPAT ? 0u : grouphash((uint32_t)(j >> 2), rk); }

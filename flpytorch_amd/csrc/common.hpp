@@ -91,6 +91,9 @@ bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n,
 size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d, const float* w,
            float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st);
+size_t rk_workspace(const flc_codec_params* prm, int64_t n, int64_t d, bool reduce);
+int rk_run(const flc_codec_params* prm, RowSrc rows, int64_t n, int64_t d, bool reduce, const float* w, float wt,
+           float* out, void* wsp, size_t ws_bytes, hipStream_t st);
 int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out,
                 hipStream_t st);
 

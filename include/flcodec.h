@@ -46,7 +46,9 @@ typedef enum {
     FLC_NATURAL = 4,
     FLC_STD_DITHERING = 5,
     FLC_NAT_DITHERING = 6,
-    FLC_TOPK = 7
+    FLC_TOPK = 7,
+    FLC_RANK_K = 8          /* k = K; rank-K truncated SVD of the A x B view (compressors.py:336-364):
+                               rocSOLVER / rocBLAS, parity to a stated tolerance */
 } flc_codec;
 
 /* p-norm used by the dithering codecs (Compressor.p, compressors.py:91, 123). */

@@ -5,8 +5,8 @@ numpy restatement of the reference codecs and reduction, op for op in fp32:
 * ``parse_spec`` / ``OracleCompressor.__init__``  — initCompressor, compressors.py:435-494,
   and the make* constructors, compressors.py:64-178.
 * ``OracleCompressor.generate``  — generateCompressPattern, compressors.py:196-216.
-* ``OracleCompressor.compress``  — compressVector, compressors.py:218-371 (rank_k excluded:
-  a dense SVD, SURVEY §8f, not on this round's path).
+* ``OracleCompressor.compress``  — compressVector, compressors.py:218-371 (rank_k: numpy's float32
+  LAPACK SVD, like torch's CPU path; its outputs match the reference to a tolerance, not bits).
 * ``server_gradient``            — serverGradient core, algorithms.py:1748-1770 (DCGD) and
   1810-1832 (FedAvg): gs = w0 (x - x0); gs += wi (x - xi) in buffer order; gs / sum(w).
 * ``reduce_plain``               — the fused encode+reduce contract of the product:
@@ -108,6 +108,13 @@ class OracleCompressor:
         elif name == "topk":
             self.type, self.K = TOPK, kspec(params[1])
             self.alpha = self.K / D
+        elif name == "rank_k":                        # makeRankKCompressor, compressors.py:151-172
+            self.type, self.K = RANK_K, kspec(params[1])
+            a = int(D ** 0.5)
+            while D % a != 0:
+                a += 1
+            self.A, self.B = a, D // a
+            self.alpha = self.K / min(self.A, self.B)
         else:
             raise AssertionError("Unknown compressor format")   # compressors.py:492
 
@@ -185,8 +192,13 @@ class OracleCompressor:
                 ind = topk_indices(x, self.K)
                 out[ind] = x[ind]
                 need = self.K
+            elif t == RANK_K:                         # compressors.py:336-364
+                U, S, Vt = np.linalg.svd(x.reshape(self.A, self.B), full_matrices=False)
+                K = min(len(S), self.K)
+                out = ((U[:, :K] * S[:K]) @ Vt[:K, :]).astype(_F32).reshape(d)
+                need = K * (self.A + self.B)
             else:
-                raise NotImplementedError("rank_k is not part of the oracle")
+                raise NotImplementedError(f"codec {t}")
         self.last_input_advance = d
         self.last_need_to_send_advance = need
         self.really_need_to_send_components += need

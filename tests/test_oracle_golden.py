@@ -151,3 +151,23 @@ def test_run_patterns_follow_stream():
             np.testing.assert_array_equal(rs.choice(D, K), pats[k])
             rs.randint31()
             k += 1
+
+
+RK_META, RK = load("rank_k")
+# Rank-K (compressors.py:336-364) goes through a floating-point SVD: the oracle (numpy LAPACK, fp32)
+# and the reference (torch LAPACK, fp32) agree to rounding, not bits.  Tolerance on the error norm,
+# relative to the input norm:
+RANK_K_RTOL = 1e-5
+
+
+@pytest.mark.parametrize("i", range(len(RK_META)), ids=[f"{m['spec']}-{m['D']}" for m in RK_META])
+def test_rank_k_golden(i):
+    m = RK_META[i]
+    x, want = RK[f"x{i}"], RK[f"y{i}"]
+    comp = oc.OracleCompressor(m["spec"], m["D"])
+    assert (comp.A, comp.B, comp.K, comp.alpha) == (m["A"], m["B"], m["K"], m["alpha"])
+    out = comp.compress(x)
+    assert out.dtype == np.float32 and out.shape == want.shape
+    err = float(np.linalg.norm(out.astype(np.float64) - want)) / max(float(np.linalg.norm(x)), 1e-30)
+    assert err <= RANK_K_RTOL, err
+    assert comp.last_need_to_send_advance == m["need"]
