@@ -25,6 +25,7 @@ EXPORTS = [
     "flc_reduce_rows", "flc_reduce_matrix",
     "flc_encode_workspace_size", "flc_encode",
     "flc_encode_reduce_workspace_size", "flc_encode_reduce",
+    "flc_encode_shift_workspace_size", "flc_encode_shift",
     "flc_mt_choice", "flc_mt_rand", "flc_mt_randint31",
     "flc_device_uniform", "flc_device_randk_indices",
     "flc_profile_enable", "flc_profile_collect",
@@ -91,6 +92,10 @@ def load():
         lib.flc_encode_reduce_workspace_size.restype = sz
         lib.flc_encode_reduce.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, i64, i64, vp, f32, vp, vp,
                                           vp, sz, vp]
+        lib.flc_encode_shift_workspace_size.argtypes = [P(FlcCodecParams), i64]
+        lib.flc_encode_shift_workspace_size.restype = sz
+        lib.flc_encode_shift.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, vp, i64, f32, vp, vp, f32, vp, vp, vp,
+                                         vp, sz, vp]
         lib.flc_mt_choice.argtypes = [vp, vp, i64, i64, vp, vp]
         lib.flc_mt_rand.argtypes = [vp, vp, i64, vp]
         lib.flc_mt_randint31.argtypes = [vp, vp, i64, vp]
@@ -102,7 +107,8 @@ def load():
         lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
         for name in EXPORTS:
             if name not in ("flc_version", "flc_last_error_string", "flc_device_uniform",
-                            "flc_encode_workspace_size", "flc_encode_reduce_workspace_size"):
+                            "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
+                            "flc_encode_shift_workspace_size"):
                 getattr(lib, name).restype = i32
         _lib = lib
         return lib

@@ -282,42 +282,40 @@ class Compressor:
             prm.seed = int(self.device_rng[0]) & 0xFFFFFFFFFFFFFFFF
         return prm, keep
 
-    def compressVector(self, x):
-        d = max(x.shape)
-        self.last_input_advance = d
-        self.last_need_to_send_advance = 0
+    def _need_to_send(self, d):
+        """Wire count of one call (compressors.py:227-364, the last_need_to_send_advance lines)."""
         t = self.compressorType
         if t == CompressorType.IDENTICAL:
-            out = x                                                     # alias, like the reference
-            self.last_need_to_send_advance = d
-        elif t == CompressorType.RANK_K_COMPRESSOR:
-            out = self._encode_gpu(x)
+            return d
+        if t == CompressorType.LAZY_COMPRESSOR:
+            return d if self.testp < self.P else 0
+        if t in (CompressorType.RANDK_COMPRESSOR, CompressorType.TOPK_COMPRESSOR):
+            return self.K
+        if t == CompressorType.NATURAL_COMPRESSOR_FP32:
+            return 9.0 / 32.0 * d
+        if t == CompressorType.RANK_K_COMPRESSOR:
             # only the dyadic expansion is sent: K' (A + B), K' = min(K, min(A, B)) (compressors.py:348, 362)
-            self.last_need_to_send_advance = min(self.K, self.A, self.B) * (self.A + self.B)
-        else:
-            out = self._encode_gpu(x)
-            if t == CompressorType.LAZY_COMPRESSOR:
-                self.last_need_to_send_advance = d if self.testp < self.P else 0
-            elif t in (CompressorType.RANDK_COMPRESSOR, CompressorType.TOPK_COMPRESSOR):
-                self.last_need_to_send_advance = self.K
-            elif t == CompressorType.NATURAL_COMPRESSOR_FP32:
-                self.last_need_to_send_advance = 9.0 / 32.0 * d
-            else:
-                self.last_need_to_send_advance = 1.0 + d * (1.0 + math.ceil(math.log2(self.s))) / 32.0
+            return min(self.K, self.A, self.B) * (self.A + self.B)
+        return 1.0 + d * (1.0 + math.ceil(math.log2(self.s))) / 32.0
+
+    def _account(self, d):
+        self.last_input_advance = d
+        self.last_need_to_send_advance = self._need_to_send(d)
         self.really_need_to_send_components += self.last_need_to_send_advance
         self.total_input_components += self.last_input_advance
+
+    def compressVector(self, x):
+        d = max(x.shape)
+        if self.compressorType == CompressorType.IDENTICAL:
+            out = x                                                     # alias, like the reference
+        else:
+            out = self._encode_gpu(x)
+        self._account(d)
         return out
 
-    def _encode_gpu(self, x, pnorm_in=None, pnorm_out=None):
-        if x.dtype != torch.float32:
-            raise TypeError(f"flcodec encodes fp32 only (got {x.dtype})")
-        dev = _gpu_device(x)
-        host_in = not x.is_cuda
-        xd = x.reshape(-1).to(device=dev).contiguous()
-        d = xd.numel()
+    def _pattern(self, dev, keep):
+        """flc_pattern for this compressor's current pattern (compat mode) or device-RNG key."""
         t = self.compressorType
-        lib = _lib.load()
-        prm, keep = self.codec_params(dev)
         pat = _lib.FlcPattern()
         if self.device_rng is not None:
             pat.client0 = int(self.device_rng[1])
@@ -337,6 +335,18 @@ class Compressor:
             if self.testp.device != dev:
                 self.testp = self.testp.to(device=dev, non_blocking=True)
             pat.d_uniforms = self.testp.data_ptr()
+        return pat
+
+    def _encode_gpu(self, x, pnorm_in=None, pnorm_out=None):
+        if x.dtype != torch.float32:
+            raise TypeError(f"flcodec encodes fp32 only (got {x.dtype})")
+        dev = _gpu_device(x)
+        host_in = not x.is_cuda
+        xd = x.reshape(-1).to(device=dev).contiguous()
+        d = xd.numel()
+        lib = _lib.load()
+        prm, keep = self.codec_params(dev)
+        pat = self._pattern(dev, keep)
         out = torch.empty_like(xd)
         ws_bytes = lib.flc_encode_workspace_size(ctypes.byref(prm), d)
         ws = _lib.WORKSPACE.get(dev, ws_bytes)
@@ -349,6 +359,74 @@ class Compressor:
         _lib.check(rc, "flc_encode")
         out = out.reshape(x.shape)
         return out.to("cpu") if host_in else out
+
+    # -- shift codecs ----------------------------------------------------
+    def compressShift(self, a, b, *, scale=1.0, base=None, out=None, alpha=None, shift=None, shift_out=None,
+                      message=True, pnorm_out=None):
+        """One fused pass of ``base + compressVector(a - b) * scale`` and ``shift + alpha * C(a - b)``.
+
+        The torch expressions of the compressed algorithms' client step (DIANA algorithms.py:1383-1391,
+        EF21 1506-1517, MARINA 537 / 691, FRECON 1104-1110, COFIG 1265-1269), fp32 op for op: the
+        scalars are taken as fp32, like torch's tensor-scalar ops.  Returns ``(msg, shift_out)``
+        (``msg`` None when ``message`` is False, ``shift_out`` None without ``alpha``).  ``out`` /
+        ``shift_out`` may be any of the inputs (in-place update).  Updates the wire statistics
+        like ``compressVector``.  Device tensors only (the client state lives on the GPU)."""
+        for name, v in (("a", a), ("b", b), ("base", base), ("shift", shift), ("out", out),
+                        ("shift_out", shift_out)):
+            if v is not None and (v.dtype != torch.float32 or not v.is_cuda):
+                raise TypeError(f"compressShift: {name} must be an fp32 device tensor")
+        dev = _gpu_device(a)
+        d = a.numel()
+        if b.numel() != d or (base is not None and base.numel() != d) or (shift is not None and shift.numel() != d):
+            raise ValueError("compressShift: a, b, base and shift must have the same number of elements")
+        if alpha is not None and shift is None:
+            raise ValueError("compressShift: alpha given without a shift tensor")
+        keep = []
+
+        def flat(v):
+            if v is None:
+                return None
+            f = v.reshape(-1)
+            if not f.is_contiguous():
+                f = f.contiguous()
+            keep.append(f)
+            return f
+        af, bf, basef, hf = flat(a), flat(b), flat(base), flat(shift)
+        msg = None
+        if message:
+            msg = out if out is not None else torch.empty_like(af)
+            if not msg.is_contiguous():
+                raise ValueError("compressShift: out must be contiguous")
+        hout = None
+        if alpha is not None:
+            hout = shift_out if shift_out is not None else torch.empty_like(hf)
+            if not hout.is_contiguous():
+                raise ValueError("compressShift: shift_out must be contiguous")
+        if msg is None and hout is None:
+            raise ValueError("compressShift: nothing to compute (message=False and no alpha)")
+        lib = _lib.load()
+        prm, k2 = self.codec_params(dev)
+        keep.extend(k2)
+        pat = self._pattern(dev, keep)
+        ws_bytes = lib.flc_encode_shift_workspace_size(ctypes.byref(prm), d)
+        ws = _lib.WORKSPACE.get(dev, ws_bytes)
+        vp = ctypes.c_void_p
+
+        def ptr(v):
+            return vp(v.data_ptr() if v is not None else None)
+        with torch.cuda.device(dev):
+            rc = lib.flc_encode_shift(ctypes.byref(prm), ctypes.byref(pat), ptr(af), ptr(bf), d,
+                                      ctypes.c_float(float(np.float32(scale))), ptr(basef), ptr(msg),
+                                      ctypes.c_float(float(np.float32(alpha if alpha is not None else 0.0))),
+                                      ptr(hf if hout is not None else None), ptr(hout), ptr(pnorm_out),
+                                      vp(ws.data_ptr()), ws.numel(), _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_encode_shift")
+        self._account(d)
+        if msg is not None:
+            msg = msg.view(a.shape)
+        if hout is not None:
+            hout = hout.view(shift.shape)
+        return msg, hout
 
 
 def initCompressor(compressorCmdLine, D):

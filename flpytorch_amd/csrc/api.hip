@@ -150,6 +150,25 @@ extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, c
     }
 }
 
+extern "C" size_t flc_encode_shift_workspace_size(const flc_codec_params* prm, int64_t d) {
+    if (!prm || !known(prm->codec) || d < 0) return 0;
+    return shift_workspace(prm, d);
+}
+
+extern "C" int flc_encode_shift(const flc_codec_params* prm, const flc_pattern* pat, const float* d_a,
+                                const float* d_b, int64_t d, float msg_scale, const float* d_base, float* d_msg,
+                                float shift_alpha, const float* d_shift_in, float* d_shift_out, float* d_pnorm_out,
+                                void* d_ws, size_t ws_bytes, void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_encode_shift: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (d < 0) { set_error("flc_encode_shift: d < 0"); return FLC_ERR_ARG; }
+    if (d > 0 && (!d_a || !d_b)) { set_error("flc_encode_shift: need a and b"); return FLC_ERR_ARG; }
+    if (d > 0 && !d_msg && !d_shift_out) { set_error("flc_encode_shift: nothing to write (msg and shift_out null)"); return FLC_ERR_ARG; }
+    if (d_shift_out && !d_shift_in) { set_error("flc_encode_shift: shift_out without shift_in"); return FLC_ERR_ARG; }
+    if (d_base && !d_msg) { set_error("flc_encode_shift: base without msg"); return FLC_ERR_ARG; }
+    ShiftArgs sh{d_b, msg_scale, d_base, d_msg, shift_alpha, d_shift_in, d_shift_out};
+    return shift_run(prm, pat, d_a, d, sh, d_pnorm_out, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
 extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern* pat, const float* d_rows, int64_t ld,
                                  const float* const* d_row_ptrs, int64_t n, int64_t d, const float* d_w, float w_total,
                                  float* d_pnorms_out, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {

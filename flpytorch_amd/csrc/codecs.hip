@@ -42,11 +42,14 @@ __device__ inline double ncomb(double a, double b) {
 // nonzero |v| below 2^-80: the row cannot use the unguarded fast division (div_fast)
 __device__ inline uint32_t is_tiny(float v) { const float a = fabsf(v); return (a != 0.f && a < 0x1p-80f) ? 1u : 0u; }
 
-template <int NORM, bool VEC>
-__global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, int64_t d, int64_t parts,
-                                                       double* __restrict__ partial, uint32_t* __restrict__ tinyp) {
+// DIFF: the row is the fp32 difference src.row(0) - sub (the shift codecs' C(a - b), one row)
+template <int NORM, bool VEC, bool DIFF>
+__global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, const float* __restrict__ sub, int64_t d,
+                                                       int64_t parts, double* __restrict__ partial,
+                                                       uint32_t* __restrict__ tinyp) {
     const int64_t row = blockIdx.y;
     const float* r = src.row(row);
+    auto ld1 = [&](int64_t j) -> float { return DIFF ? r[j] - sub[j] : r[j]; };
     __shared__ double red[4];
     __shared__ uint32_t redt[4];
     for (int64_t part = blockIdx.x; part < parts; part += gridDim.x) {
@@ -58,12 +61,16 @@ __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, int64_t d, in
             const int64_t g0 = j0 / 4, g1 = j1 / 4;   // j0 % 4 == 0 (NORM_PART % 4 == 0)
             for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
                 float4 v = reinterpret_cast<const float4*>(r)[g];
+                if (DIFF) {
+                    const float4 u = reinterpret_cast<const float4*>(sub)[g];
+                    v = make_float4(v.x - u.x, v.y - u.y, v.z - u.z, v.w - u.w);
+                }
                 a = nacc<NORM>(a, v.x); a = nacc<NORM>(a, v.y); a = nacc<NORM>(a, v.z); a = nacc<NORM>(a, v.w);
                 tiny |= is_tiny(v.x) | is_tiny(v.y) | is_tiny(v.z) | is_tiny(v.w);
             }
-            for (int64_t j = g1 * 4 + threadIdx.x; j < j1; j += 256) { a = nacc<NORM>(a, r[j]); tiny |= is_tiny(r[j]); }
+            for (int64_t j = g1 * 4 + threadIdx.x; j < j1; j += 256) { const float v = ld1(j); a = nacc<NORM>(a, v); tiny |= is_tiny(v); }
         } else {
-            for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) { a = nacc<NORM>(a, r[j]); tiny |= is_tiny(r[j]); }
+            for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) { const float v = ld1(j); a = nacc<NORM>(a, v); tiny |= is_tiny(v); }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -115,7 +122,8 @@ int64_t norm_parts(int64_t d) { return (d + NORM_PART - 1) / NORM_PART; }
 
 int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* partial, uint32_t* tinyp,
                  float* pn, float* rpn, uint32_t* rowfast, uint64_t seed, int64_t client0, uint32_t* rk,
-                 hipStream_t st) {
+                 hipStream_t st, const float* sub) {
+    if (sub && n != 1) { set_error("launch_norms: a difference source is one row"); return FLC_ERR_ARG; }
     const int64_t parts = norm_parts(d);
     if (n == 0) return FLC_OK;
     if (parts == 0) {  // d == 0: norm of an empty vector
@@ -127,8 +135,10 @@ int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* p
     dim3 grid((unsigned)std::min<int64_t>(parts, 64), (unsigned)n);
 #define FLC_NORM_CASE(NK)                                                                           \
     { ProfScope _ps("k_norm_partials", st);                                                         \
-    if (vec) hipLaunchKernelGGL((k_norm_partials<NK, true>), grid, dim3(256), 0, st, src, d, parts, partial, tinyp); \
-    else hipLaunchKernelGGL((k_norm_partials<NK, false>), grid, dim3(256), 0, st, src, d, parts, partial, tinyp); } \
+    if (sub && vec) hipLaunchKernelGGL((k_norm_partials<NK, true, true>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); \
+    else if (sub) hipLaunchKernelGGL((k_norm_partials<NK, false, true>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); \
+    else if (vec) hipLaunchKernelGGL((k_norm_partials<NK, true, false>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); \
+    else hipLaunchKernelGGL((k_norm_partials<NK, false, false>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); } \
     FLC_CHECK_LAUNCH("k_norm_partials");                                                            \
     hipLaunchKernelGGL((k_norm_final<NK>), dim3((unsigned)n), dim3(64), 0, st, partial, tinyp, parts, n, pn, rpn,   \
                        rowfast, seed, client0, rk);                                                 \
@@ -163,6 +173,60 @@ __global__ __launch_bounds__(256) void k_ew_dense(const float* __restrict__ x, i
     }
     for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
         out[j] = op.template apply<false>(x[j], j, op.col(j), smem_tab);
+}
+
+// ------------------------------------------------------------------------------------------
+// Shift codecs, one row (algorithms.py DIANA 1383-1391, EF21 1506-1517, MARINA
+// 537 / 691, FRECON 1104-1110, COFIG 1265-1269): e = C(a - b) is never stored —
+//     msg   = base + e * scale   (or e * scale without a base)
+//     h_out = h_in + alpha * e
+// each op rounded separately in fp32 (torch scalar ops on fp32 tensors take the scalar as fp32).
+// Every element is read and written by one thread, so msg / h_out may alias a, b, base or h_in.
+// ------------------------------------------------------------------------------------------
+__device__ inline void shift_epi1(const ShiftArgs& sh, int64_t j, float e) {
+    if (sh.msg) {
+        const float t = e * sh.scale;
+        sh.msg[j] = sh.base ? sh.base[j] + t : t;
+    }
+    if (sh.hout) sh.hout[j] = sh.hin[j] + sh.alpha * e;
+}
+
+template <class Op, bool VEC>
+__global__ __launch_bounds__(256) void k_ew_shift(const float* __restrict__ a, int64_t d, Op op,
+                                                  const float* __restrict__ levels, int s, ShiftArgs sh) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem_tab[];
+    if (Op::TABLE) op.set_table_ok(load_table(levels, s, smem_tab));
+    op.setup(0);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t j0 = VEC ? (d / 4) * 4 : 0;
+    if (VEC) {
+        for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < d / 4; g += stride) {
+            uint32_t cs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cs[q] = op.col(g * 4 + q);
+            const float4 x = reinterpret_cast<const float4*>(a)[g];
+            const float4 y = reinterpret_cast<const float4*>(sh.b)[g];
+            const float4 v = make_float4(x.x - y.x, x.y - y.y, x.z - y.z, x.w - y.w);
+            const float4 e = op.row_fast() ? apply4<true>(op, v, g * 4, cs, smem_tab)
+                                           : apply4<false>(op, v, g * 4, cs, smem_tab);
+            if (sh.msg) {
+                const float4 t = make_float4(e.x * sh.scale, e.y * sh.scale, e.z * sh.scale, e.w * sh.scale);
+                float4 m = t;
+                if (sh.base) {
+                    const float4 bs = reinterpret_cast<const float4*>(sh.base)[g];
+                    m = make_float4(bs.x + t.x, bs.y + t.y, bs.z + t.z, bs.w + t.w);
+                }
+                reinterpret_cast<float4*>(sh.msg)[g] = m;
+            }
+            if (sh.hout) {
+                const float4 h = reinterpret_cast<const float4*>(sh.hin)[g];
+                reinterpret_cast<float4*>(sh.hout)[g] =
+                    make_float4(h.x + sh.alpha * e.x, h.y + sh.alpha * e.y, h.z + sh.alpha * e.z, h.w + sh.alpha * e.w);
+            }
+        }
+    }
+    for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
+        shift_epi1(sh, j, op.template apply<false>(a[j] - sh.b[j], j, op.col(j), smem_tab));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -280,6 +344,22 @@ static int launch_dense(const float* x, int64_t d, Op op, const float* levels, i
     return FLC_OK;
 }
 
+template <class Op>
+static int launch_shift(const float* a, int64_t d, Op op, const float* levels, int s, const ShiftArgs& sh,
+                        hipStream_t st) {
+    if (d == 0) return FLC_OK;
+    const uintptr_t al = (uintptr_t)a | (uintptr_t)sh.b | (uintptr_t)sh.base | (uintptr_t)sh.msg |
+                         (uintptr_t)sh.hin | (uintptr_t)sh.hout;
+    const bool vec = (al & 15u) == 0;
+    const size_t lds = Op::TABLE ? (size_t)s * sizeof(float4) : 0;
+    const int grid = grid_cap(vec ? (d + 3) / 4 : d, 256, 4096);
+    ProfScope _ps("k_ew_shift", st);
+    if (vec) hipLaunchKernelGGL((k_ew_shift<Op, true>), dim3(grid), dim3(256), lds, st, a, d, op, levels, s, sh);
+    else hipLaunchKernelGGL((k_ew_shift<Op, false>), dim3(grid), dim3(256), lds, st, a, d, op, levels, s, sh);
+    FLC_CHECK_LAUNCH("k_ew_shift");
+    return FLC_OK;
+}
+
 // tile shape of the accumulate kernel: COLS float4 columns per thread, PF rows in flight;
 // FLC_EW_TILE=<cols>x<pf> overrides (tuning runs only).
 static int ew_tile_variant() {
@@ -384,12 +464,14 @@ static int check_dither(const flc_codec_params* prm) {
 // One row encode (compressVector) or fused reduce over n rows (n >= 1).
 int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool vec, int64_t n, int64_t d,
            const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt,
-           void* ws, size_t ws_bytes, hipStream_t st) {
+           void* ws, size_t ws_bytes, hipStream_t st, const ShiftArgs* sh) {
+    if (sh && (!dense || n != 1)) { set_error("ew_run: the shift form is one dense row"); return FLC_ERR_ARG; }
     const int codec = prm->codec;
     const bool compat = pat && pat->d_uniforms;
     const int64_t client0 = pat ? pat->client0 : 0;
     UniformSrc us{compat ? pat->d_uniforms : nullptr, (pat && pat->uniforms_ld) ? pat->uniforms_ld : d};
     auto go = [&](auto op, const float* levels, int s) -> int {
+        if (sh) return launch_shift(src.base, d, op, levels, s, *sh, st);
         if (dense) return launch_dense(src.base, d, op, levels, s, out, st);
         return launch_accum(src, vec, n, d, op, levels, s, w, wt, out, st);
     };
@@ -425,7 +507,7 @@ int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool
             RowTabs rt{pnorm_in, nullptr, nullptr, e.rk};
             if (!pnorm_in) {
                 rc = launch_norms(src, vec, n, d, prm->norm, e.partial, e.tinyp, e.pn, e.rpn, e.fast, prm->seed,
-                                  client0, e.rk, st);
+                                  client0, e.rk, st, sh ? sh->b : nullptr);
                 if (rc) return rc;
                 rt = RowTabs{e.pn, e.rpn, e.fast, e.rk};
             } else if (!compat) {

@@ -81,9 +81,23 @@ struct RowSrc {
 int reduce_impl(RowSrc src, bool rows_vec_ok, int64_t n, int64_t d, const float* x, const float* w, float wt,
                 int mode, float* out, hipStream_t st);
 size_t ew_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+// The shift codecs' epilogue (flc_encode_shift): b is subtracted from the input row before the
+// codec; msg = base + C * scale, hout = hin + alpha * C (null msg / hout: not written).
+struct ShiftArgs {
+    const float* b;
+    float scale;
+    const float* base;
+    float* msg;
+    float alpha;
+    const float* hin;
+    float* hout;
+};
 int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool vec, int64_t n, int64_t d,
            const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt, void* ws,
-           size_t ws_bytes, hipStream_t st);
+           size_t ws_bytes, hipStream_t st, const ShiftArgs* sh = nullptr);
+size_t shift_workspace(const flc_codec_params* prm, int64_t d);
+int shift_run(const flc_codec_params* prm, const flc_pattern* pat, const float* a, int64_t d, const ShiftArgs& sh,
+              float* pnorm_out, void* ws, size_t ws_bytes, hipStream_t st);
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st);

@@ -137,6 +137,29 @@ int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern* pat, const
                       void* d_ws, size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------------------------------------
+ * Shift codecs — the client-side update of the compressed algorithms,
+ * one client row, with e = C(a - b) never stored for the elementwise codecs:
+ *     d_msg       = d_base + e * msg_scale        (e * msg_scale when d_base == NULL)
+ *     d_shift_out = d_shift_in + shift_alpha * e
+ * each op rounded separately in fp32, like the torch expressions it replaces:
+ *   DIANA  m = C(g - h); h = h + alpha * m              algorithms.py:1383-1391
+ *          -> a=g, b=h, msg_scale=1, msg=m, shift_in=h, shift_out=h', alpha=(float)alpha
+ *   EF21   g_next = g_prev + C(g - g_prev) * mult      algorithms.py:1506-1517
+ *          -> a=g, b=g_prev, base=g_prev, msg_scale=(float)mult, msg=g_next
+ *   MARINA g_next = g_prev + C(g - g_prev_x)           algorithms.py:537, 691
+ *   FRECON / COFIG u = C(g - h); h = h + alpha * u     algorithms.py:1104-1110, 1265-1269
+ * C follows prm / pat exactly as in flc_encode (same patterns, same draws).  d_msg or
+ * d_shift_out may be NULL (not written), not both; outputs may alias any input (every element
+ * is read before it is written, by the same thread).  d_pnorm_out: optional norm of a - b
+ * (dithering).
+ * -------------------------------------------------------------------------------------- */
+size_t flc_encode_shift_workspace_size(const flc_codec_params* prm, int64_t d);
+int flc_encode_shift(const flc_codec_params* prm, const flc_pattern* pat, const float* d_a,
+                     const float* d_b, int64_t d, float msg_scale, const float* d_base, float* d_msg,
+                     float shift_alpha, const float* d_shift_in, float* d_shift_out,
+                     float* d_pnorm_out, void* d_ws, size_t ws_bytes, void* stream);
+
+/* ----------------------------------------------------------------------------------------
  * Host side of compat mode: the numpy legacy MT19937 stream (what the reference's
  * rndgen.choice / rand / random / randint draw, compressors.py:204-212, algorithms.py:2055),
  * advanced in place on a caller-held state (key[624], pos — numpy's get_state() layout).

@@ -244,3 +244,20 @@ def reduce_plain(rows, weights=None):
         wt += w[i]
         gs = gs + _F32(w[i]) * np.asarray(rows[i], dtype=_F32)
     return gs / _F32(wt)
+
+
+def shift_step(comp, a, b, scale=1.0, base=None, alpha=None, h=None, pnorm=None):
+    """The shift codecs' client step, fp32 op for op as the torch expressions:
+    e = C(a - b); msg = base + e * scale (e * scale without base); h' = h + alpha * e.
+    DIANA algorithms.py:1383-1391 (scale 1, no base, h += alpha m), EF21 1506-1517
+    (base = b = g_prev, scale = 1 / (1 + w) or 1), MARINA 537 / 691 (base = g_prev),
+    FRECON 1104-1110, COFIG 1265-1269.  Python scalars enter as fp32 (torch's tensor-scalar ops)."""
+    with np.errstate(all="ignore"):
+        diff = (np.asarray(a, dtype=_F32) - np.asarray(b, dtype=_F32)).astype(_F32)
+        e = comp.compress(diff, pnorm=pnorm)
+        t = (e * _F32(scale)).astype(_F32)
+        msg = t if base is None else (np.asarray(base, dtype=_F32) + t).astype(_F32)
+        h2 = None
+        if alpha is not None:
+            h2 = (np.asarray(h, dtype=_F32) + (_F32(alpha) * e).astype(_F32)).astype(_F32)
+    return msg, h2

@@ -171,3 +171,26 @@ def test_rank_k_golden(i):
     err = float(np.linalg.norm(out.astype(np.float64) - want)) / max(float(np.linalg.norm(x)), 1e-30)
     assert err <= RANK_K_RTOL, err
     assert comp.last_need_to_send_advance == m["need"]
+
+
+SH_META, SH = load("shift")
+
+
+@pytest.mark.parametrize("i", range(len(SH_META)), ids=[f"{m['algo']}-{m['spec']}-{m['D']}" for m in SH_META])
+def test_shift_step_golden(i):
+    """The shift codecs' client step (DIANA / EF21 / MARINA) against the reference codecs driven by
+    the algorithms' own torch expressions: bit-exact (dithering given the reference's norm)."""
+    from tests.golden_io import shift_fingerprint, shift_inputs
+    m = SH_META[i]
+    a, b, x3 = shift_inputs(m["seed"], m["D"])
+    assert shift_fingerprint(a, b, x3) == m["fingerprint"]
+    comp = oc.OracleCompressor(m["spec"], m["D"])
+    comp.generate(OracleRandomState(m["seed"]))
+    base = {"b": b, "x3": x3, None: None}[m["base"]]
+    pn = m["pnorm"] if comp.type in (oc.STD_DITHERING, oc.NAT_DITHERING) else None
+    msg, h2 = oc.shift_step(comp, a, b, scale=m["scale"], base=base, alpha=m["alpha"],
+                            h=b if m["alpha"] is not None else None, pnorm=pn)
+    np.testing.assert_array_equal(msg.view(np.uint32), SH[f"msg{i}"].view(np.uint32))
+    if m["alpha"] is not None:
+        np.testing.assert_array_equal(h2.view(np.uint32), SH[f"h{i}"].view(np.uint32))
+    assert comp.last_need_to_send_advance == m["need"]
