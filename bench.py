@@ -13,6 +13,9 @@ Workloads (BASELINE.json configs; the default is the largest single-GPU config, 
   c3  topk:1%   N=1024 / GPU, D=10 M   (ResNet-18-sized)                     [default]
   c2  randk:1%  N=256  / GPU, D=1 M    (device-RNG indices)
   c4  qsgd:127  N=512  / GPU, D=25 M   (C4's per-GPU shard: at --gpus 8 this IS C4, N=4096)
+  c5  randk:1% / topk:1% / qsgd:127 by client id mod 3, N=2048 / GPU, D=100 M (at --gpus 8: N=16384);
+      48 resident distinct rows replayed through the clients' row pointers; the per-group [D]
+      partials are all-reduced asynchronously, overlapping the next group's encode
   reduce  ident N=512 / GPU, D=25 M   (the serverGradient fold alone)
 
 Algorithmic bytes: topk / qsgd / ident 4*N*D + 4*D; randk 4*N*K + 4*D (device-RNG
@@ -42,16 +45,30 @@ PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level paramet
 WORKLOADS = {
     "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2,
                others=["k_topk_sample", "k_cand_select", "k_chunk_accum"]),
-    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_scatter", config=1, others=["k_chunk_accum"]),
+    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_coarse", config=1,
+               others=["k_chunk_accum"]),
     # sparse QSGD path (dither_sparse.hip): one read of every row in k_ds_filter
     "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3,
                others=["k_ds_sample", "k_ds_accum"]),
+    # C5: mixed per-client codec (client i -> specs[i % 3]); a pool of resident distinct rows is
+    # replayed through the clients' row pointers (819 GB of distinct rows per GPU would not fit)
+    "c5": dict(spec="mixed", specs=["randk:1%", "topk:1%", "qsgd:127"], n=2048, d=100_000_000, pool=48,
+               kernel="k_ds_filter", config=4,
+               others=["k_topk_filter", "k_randk_coarse", "k_randk_fine", "k_ds_accum", "k_chunk_accum"]),
     # the serverGradient fold alone (identity codec), C4's shard shape
     "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3, others=[]),
 }
 
 
-def algorithmic_bytes(spec, n, d, k):
+def algorithmic_bytes(spec, n, d, k, specs=None):
+    if specs:                                  # mixed: client i uses specs[i % G]; one [D] result
+        G = len(specs)
+        total = 4 * d
+        for g, sp in enumerate(specs):
+            ng = len(range(g, n, G))
+            kg = math.ceil(0.01 * d)
+            total += algorithmic_bytes(sp, ng, d, kg) - 4 * d
+        return total
     if spec.startswith("randk"):
         return 4 * n * k + 4 * d
     return 4 * n * d + 4 * d
@@ -59,15 +76,16 @@ def algorithmic_bytes(spec, n, d, k):
 
 def kernel_bytes(kernel, n, d, k):
     """Algorithmic bytes one launch of the dominant kernel must move."""
-    if kernel == "k_randk_scatter":
-        return 8 * n * k            # gather K values per row + write K (idx, value) entries
+    if kernel == "k_randk_coarse":
+        return 8 * n * k            # C2 (one chunk per superchunk): sample, bucket, gather K values per row + write them
     if kernel in ("k_ew_accum_vec", "k_reduce_vec"):
         return 4 * n * d + 4 * d    # read every row once, write the [D] result
     return 4 * n * d                # k_topk_filter / k_ds_filter: read every row once
 
 
-def cpu_baseline(spec, d, budget_s=12.0):
-    """Oracle (numpy, 1 core) encode + sequential reduce of a bounded sample of rows."""
+def cpu_baseline(spec, d, budget_s=12.0, specs=None):
+    """Oracle (numpy, 1 core) encode + sequential reduce of a bounded sample of rows (mixed: the
+    rows cycle through the constituent codecs like the clients do)."""
     from oracle import codecs as oc
     from oracle.rng import OracleRandomState
     g = np.random.default_rng(0)
@@ -77,7 +95,7 @@ def cpu_baseline(spec, d, budget_s=12.0):
     acc = None
     while True:
         x = g.standard_normal(d).astype(np.float32)
-        o = oc.OracleCompressor(spec, d)
+        o = oc.OracleCompressor(specs[rows % len(specs)] if specs else spec, d)
         o.generate(rs)
         rs.randint31()
         e = o.compress(x)
@@ -87,9 +105,9 @@ def cpu_baseline(spec, d, budget_s=12.0):
             break
     dt = time.perf_counter() - t0
     k = math.ceil(0.01 * d)
-    return {"value": round(algorithmic_bytes(spec, rows, d, k) / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+    return {"value": round(algorithmic_bytes(spec, rows, d, k, specs) / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
             "kind": "port",
-            "sample": f"oracle/codecs.py {spec}: pattern + encode + sequential fp32 reduce of {rows} rows x D={d} "
+            "sample": f"oracle/codecs.py {'/'.join(specs) if specs else spec}: pattern + encode + sequential fp32 reduce of {rows} rows x D={d} "
                       f"({dt:.1f} s, numpy single-threaded)"}
 
 
@@ -188,25 +206,36 @@ def main():
     from flpytorch_amd import aggregation as ag
 
     n, d, spec = wl["n"], wl["d"], wl["spec"]
-    comp = ag.initCompressor(spec, d)
-    k = getattr(comp, "K", 0) or 0
+    specs = wl.get("specs")
+    mixed = specs is not None
+    k = math.ceil(0.01 * d) if mixed else (getattr(ag.initCompressor(spec, d), "K", 0) or 0)
     # synthetic rows ~ N(0, 1) fp32, seeded per rank (device generator; never leaves HBM)
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    rows = torch.empty((n, d), dtype=torch.float32, device=dev)
-    for i in range(0, n, 64):
+    n_dist = min(n, wl["pool"]) if mixed else n
+    rows = torch.empty((n_dist, d), dtype=torch.float32, device=dev)
+    for i in range(0, n_dist, 64):
         rows[i:i + 64].normal_(generator=gen)
     out = torch.empty(d, dtype=torch.float32, device=dev)
-    red = ag.UplinkReducer(comp, device=dev, seed=20241015)
     client0 = rank * n
+    if mixed:
+        row_list = [rows[i % n_dist] for i in range(n)]
+        up = ag.MixedUplink(specs, d, seed=20241015, device=dev)
+        group = None
+        if world > 1:
+            group = dist.group.WORLD
+    else:
+        red = ag.UplinkReducer(ag.initCompressor(spec, d), device=dev, seed=20241015)
 
-    if world > 1:
+    if world > 1 and not mixed:
         from flpytorch_amd.sharding import ShardedUplink, product_partial
         # local partial = sum_i C_i(row_i) in client order (fp32 divisor 1.0 keeps it exact),
         # one RCCL all-reduce of D floats over xGMI, then the global mean
         uplink = ShardedUplink(product_partial(red), mode="allreduce")
 
     def step():
-        if world == 1:
+        if mixed:
+            up(row_list, client0=client0, total_weight=float(n * world), out=out, group=group)
+        elif world == 1:
             red(rows, out=out, client0=client0)
         else:
             uplink(rows, client0=client0, total_weight=float(n * world), out=out)
@@ -240,11 +269,12 @@ def main():
         elapsed = float(t.item())
 
     step_ms = elapsed / args.steps * 1e3
-    total_bytes = algorithmic_bytes(spec, n, d, k) * world
+    total_bytes = algorithmic_bytes(spec, n, d, k, specs) * world
     value = total_bytes / (elapsed / args.steps) / 1e9
     # the dominant kernel may run as several launches per step (sparse QSGD: one per row group):
     # its achieved rate is the algorithmic bytes of a step over its summed launch time per step
-    kb = kernel_bytes(wl["kernel"], n, d, k)
+    # mixed: the dominant kernel serves the qsgd group only
+    kb = kernel_bytes(wl["kernel"], len(range(specs.index("qsgd:127"), n, len(specs))) if mixed else n, d, k)
     kavg_ms = kms / max(klaunch, 1)
     kstep_ms = kms / args.steps
     achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
@@ -255,7 +285,7 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d)
+        cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d, budget_s=20.0 if mixed else 12.0, specs=specs)
         line = {
             "metric": "gradient-codec encode+reduce GB/s (device-resident), [N,D] fp32; % HBM peak",
             "value": round(value, 2),
@@ -268,8 +298,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic N(0,1) fp32 rows generated on device (seeded per rank); device-RNG patterns",
-            "config": {"workload": f"C{wl['config'] + 1} {spec} N={n}/GPU D={d}", "codec": spec,
+            "data": "synthetic N(0,1) fp32 rows generated on device (seeded per rank); device-RNG patterns"
+                    + (f"; {n_dist} resident distinct rows replayed through the {n} clients' row pointers, "
+                       "each client its own codec (client id mod 3) and device-RNG key" if mixed else ""),
+            "config": {"workload": f"C{wl['config'] + 1} {'/'.join(specs) if mixed else spec} N={n}/GPU D={d}",
+                       "codec": "/".join(specs) if mixed else spec,
                        "clients_per_gpu": n, "clients_total": n * world, "D": d, "K": k,
                        "parallelism": f"client-shard dp{world}" + (" + RCCL all-reduce" if world > 1 else "")},
             "pct_hbm_peak": round(100.0 * value / world / PEAK_GBS, 2),

@@ -14,6 +14,7 @@ Pattern sources
   * device  — counter-based draws keyed by (seed, client id, element) generated inside the
               kernels: no host work, no uniform bytes (the benchmark mode).
 """
+import contextlib
 import ctypes
 
 import torch
@@ -63,7 +64,10 @@ class UplinkReducer:
             # the pointer-array entry reads rows with 16-byte vector loads: keep them aligned
             rows = [r if (r.is_contiguous() and r.data_ptr() % 16 == 0) else r.contiguous().clone() for r in rows]
             keep.extend(rows)
-            pt = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+            # pinned staging + async copy: no host wait on the work already queued on the stream
+            host_pt = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).pin_memory()
+            with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+                pt = host_pt.to(dev, non_blocking=True)
             keep.append(pt)
             base, ld, ptrs = None, 0, pt.data_ptr()
         if out is None:

@@ -185,19 +185,21 @@ __host__ __device__ inline bool below32(uint32_t h, float p) { return h < thr32(
 // Keyed bijection on [0, d): balanced Feistel on 2h bits (4^h >= d) with cycle walking.
 // RandK device mode takes the first K images: K distinct indices drawn uniformly.
 struct Feistel {
-    uint64_t key;
+    // Balanced 4-round Feistel permutation of [0, 2^(2 half_bits)) with cycle walking into [0, d):
+    // the device-RNG RandK set of a client is {perm(t) : t < K}.  Round function: fmix32 of the
+    // half XOR a 32-bit round key (round keys from the client key by mix64).
+    uint32_t rkey[4];
     uint32_t half_bits;
     uint32_t half_mask;
     uint64_t d;
-    __host__ __device__ Feistel(uint64_t ckey, uint64_t dd) : key(ckey), d(dd) {
+    __host__ __device__ Feistel(uint64_t ckey, uint64_t dd) : d(dd) {
         uint32_t b = 1;
         while ((1ull << (2 * b)) < dd) ++b;
         half_bits = b;
         half_mask = (b >= 32) ? 0xFFFFFFFFu : ((1u << b) - 1u);
+        for (int i = 0; i < 4; ++i) rkey[i] = (uint32_t)mix64(ckey + ((uint64_t)i << 56));
     }
-    __host__ __device__ inline uint32_t round_fn(uint32_t r, int i) const {
-        return (uint32_t)mix64(key + ((uint64_t)i << 56) + r) & half_mask;
-    }
+    __host__ __device__ inline uint32_t round_fn(uint32_t r, int i) const { return fmix32(r ^ rkey[i]) & half_mask; }
     __host__ __device__ inline uint64_t once(uint64_t v) const {
         uint32_t l = (uint32_t)(v >> half_bits) & half_mask, r = (uint32_t)v & half_mask;
 #pragma unroll

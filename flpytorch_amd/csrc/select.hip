@@ -19,6 +19,8 @@
 //                    distinct within a row, so every element sees its terms in row order).
 //
 // Keys: |x| bits with the sign cleared (uint32, monotone; NaN above inf like torch.topk).
+#include <stdlib.h>
+
 #include "chunks.hpp"
 
 namespace flc {
@@ -737,18 +739,270 @@ __global__ __launch_bounds__(64) void k_randk_scan(int64_t n, int64_t d, SelWs w
     ws.rowcnt[(row) * RCS] = run;
 }
 
-__global__ __launch_bounds__(256) void k_randk_scatter(RowSrc rows, int64_t n, int64_t d, int64_t K, flc_pattern pat,
-                                                       int64_t ldi, uint64_t seed, float scale, SelWs ws) {
+// bucket the row's K indices by chunk (list order inside a chunk is free: the columns are distinct)
+__global__ __launch_bounds__(256) void k_randk_scatter(int64_t n, int64_t d, int64_t K, flc_pattern pat,
+                                                       int64_t ldi, uint64_t seed, SelWs ws) {
     const int64_t row = blockIdx.y;
     Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
-    const float* r = rows.row(row);
     for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
         const int64_t j = randk_index(pat, fe, row, t, ldi);
         const int64_t slot = (j >> CHUNK_SHIFT) * n + row;
         const uint32_t pos = ws.tab[slot].x + atomicAdd(&ws.cursor[slot], 1u);
         ws.ent_idx[row * ws.cap + pos] = (uint32_t)j;
-        ws.ent_val[row * ws.cap + pos] = scale * r[j];      // (D/K) * x[S] in fp32
     }
+}
+
+// Chunk-bucketed RandK lists in two coalesced levels (the global path above evaluates the
+// permutation twice and pays two contended global atomics and a random 4-B write per index).
+//   k_randk_coarse (one workgroup per row): j = perm(t) once, parked in the row's ent_val region;
+//     LDS counts per superchunk (SB buckets of SPC chunks), LDS scan, then each index appended to
+//     its superchunk's segment of ent_idx: SB write frontiers per row, which stay in L2.
+//   k_randk_fine (one workgroup per (superchunk, row)): counting sort of the segment by chunk with
+//     LDS counters (the segment is copied to ent_val first, scattered back inside the segment),
+//     the (offset, count) table entries, then the gather (D/K) * x[j] in ascending chunk order.
+constexpr int RK_T = 1024;
+constexpr int RK_SB = 256;                   // superchunks per row (max)
+constexpr int RK_TILE = 8192;                // indices per LDS multi-split tile (32 KB)
+
+__host__ __device__ inline int64_t rk_spc(int64_t C) { return (C + RK_SB - 1) / RK_SB; }   // chunks per superchunk
+
+// Each lane walks its own sequence t = tid, tid + RK_T, ...: one Feistel round-set per loop trip for
+// every lane, an index emitted whenever the cycle walk lands inside [0, d).  (A plain
+// `while (v >= d)` per index idles the wave on its slowest lane: ~10 trips instead of ~2.7.)
+template <class Emit>
+__device__ inline void randk_walk(const flc_pattern& pat, const Feistel& fe, int64_t row, int64_t K, int64_t ldi,
+                                  int tid, Emit emit) {
+    if (pat.d_randk_idx) {
+        for (int64_t t = tid; t < K; t += RK_T) emit(t, (uint32_t)pat.d_randk_idx[row * ldi + t]);
+        return;
+    }
+    int64_t t = tid;
+    bool live = t < K;
+    uint64_t x = (uint64_t)t;
+    while (__ballot(live) != 0ull) {
+        const uint64_t v = fe.once(x);
+        if (live) {
+            if (v < fe.d) {
+                emit(t, (uint32_t)v);
+                t += RK_T;
+                live = t < K;
+                x = (uint64_t)t;
+            } else {
+                x = v;
+            }
+        }
+    }
+}
+
+// FINAL (one chunk per superchunk, C <= RK_SB): the superchunks are the chunks, so this kernel also
+// writes the (offset, count) table and gathers the values; k_randk_fine is skipped.
+template <bool FINAL>
+__global__ __launch_bounds__(RK_T) void k_randk_coarse(RowSrc rows, int64_t n, int64_t d, int64_t K, flc_pattern pat,
+                                                       int64_t ldi, uint64_t seed, float scale, SelWs ws) {
+    __shared__ uint32_t cnt[RK_SB], tcnt[RK_SB], toff[RK_SB], gbase[RK_SB];
+    __shared__ uint32_t tile[RK_TILE];
+    const int64_t row = blockIdx.x;
+    const int64_t C = nchunks(d), spc = rk_spc(C);
+    const int tid = threadIdx.x;
+    if (tid < RK_SB) cnt[tid] = 0;
+    __syncthreads();
+    const Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
+    uint32_t* jbuf = reinterpret_cast<uint32_t*>(ws.ent_val + row * ws.cap);
+    randk_walk(pat, fe, row, K, ldi, tid, [&](int64_t t, uint32_t j) {
+        jbuf[t] = j;
+        atomicAdd(&cnt[(j >> CHUNK_SHIFT) / spc], 1u);
+    });
+    __syncthreads();
+    if (tid < 64) {                          // exclusive scan of the RK_SB counts: 4 per lane
+        uint32_t v[RK_SB / 64], loc = 0;
+#pragma unroll
+        for (int q = 0; q < RK_SB / 64; ++q) { v[q] = cnt[tid * (RK_SB / 64) + q]; loc += v[q]; }
+        uint32_t incl = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, WAVE);
+            if (tid >= o) incl += u;
+        }
+        uint32_t run = incl - loc;
+#pragma unroll
+        for (int q = 0; q < RK_SB / 64; ++q) {
+            const int b = tid * (RK_SB / 64) + q;
+            if (FINAL) {
+                if (b < C) ws.tab[(int64_t)b * n + row] = make_uint2(run, v[q]);
+            } else {
+                ws.cursor[row * RK_SB + b] = run;         // segment offsets, read by k_randk_fine
+            }
+            cnt[b] = run;
+            run += v[q];
+        }
+    }
+    __syncthreads();
+    // Append to the superchunk segments tile by tile: an LDS counting sort of RK_TILE indices, then
+    // each bucket's run of the tile is written contiguously (a scattered 4-B store per index would
+    // run at a small fraction of the store rate).  Thread tid only re-reads jbuf slots it wrote.
+    uint32_t* oi = ws.ent_idx + row * ws.cap;
+    constexpr int Q = RK_TILE / RK_T;
+    for (int64_t t0 = 0; t0 < K; t0 += RK_TILE) {
+        const int m = (int)min<int64_t>(RK_TILE, K - t0);
+        if (tid < RK_SB) tcnt[tid] = 0;
+        __syncthreads();
+        uint32_t jj[Q], rnk[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int k = tid + q * RK_T;
+            if (k < m) {
+                jj[q] = jbuf[t0 + k];
+                rnk[q] = atomicAdd(&tcnt[(jj[q] >> CHUNK_SHIFT) / spc], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {
+            uint32_t v[RK_SB / 64], loc = 0;
+#pragma unroll
+            for (int q = 0; q < RK_SB / 64; ++q) { v[q] = tcnt[tid * (RK_SB / 64) + q]; loc += v[q]; }
+            uint32_t incl = loc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o, WAVE);
+                if (tid >= o) incl += u;
+            }
+            uint32_t run = incl - loc;
+#pragma unroll
+            for (int q = 0; q < RK_SB / 64; ++q) {
+                const int b = tid * (RK_SB / 64) + q;
+                toff[b] = run;
+                gbase[b] = cnt[b];
+                cnt[b] += v[q];
+                run += v[q];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int k = tid + q * RK_T;
+            if (k < m) tile[toff[(jj[q] >> CHUNK_SHIFT) / spc] + rnk[q]] = jj[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int k = tid + q * RK_T;
+            if (k < m) {
+                const uint32_t j = tile[k];
+                const uint32_t b = (j >> CHUNK_SHIFT) / spc;
+                oi[gbase[b] + (uint32_t)k - toff[b]] = j;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        ws.thr[row] = 0;
+        ws.flags[row] = F_EXACT;
+        ws.rowcnt[row * RCS] = (uint32_t)K;
+    }
+    if (FINAL) {
+        __syncthreads();                                  // block-scope visibility of the idx writes
+        const float* r = rows.row(row);
+        float* val = ws.ent_val + row * ws.cap;
+        for (int64_t t = tid; t < K; t += RK_T) val[t] = scale * r[oi[t]];   // (D/K) * x[S] in fp32
+    }
+}
+
+// Segments up to RK_FT entries (the device sampler's ~K / RK_SB, far above any binomial tail) are
+// sorted in LDS and written back, with the values, in one coalesced sweep; a larger segment (an
+// arbitrary compat index list) takes the slower in-memory counting sort.
+constexpr int RK_FT = 8192, RK_FTHR = 512;
+__global__ __launch_bounds__(RK_FTHR) void k_randk_fine(RowSrc rows, int64_t n, int64_t d, int64_t K, float scale,
+                                                        SelWs ws) {
+    extern __shared__ uint32_t fc[];                       // [spc] counts, then offsets / cursors
+    __shared__ uint32_t wsum[RK_FTHR / 64];
+    __shared__ uint32_t tile[RK_FT];
+    const int64_t row = blockIdx.y, b = blockIdx.x;
+    const int64_t C = nchunks(d), spc = rk_spc(C);
+    const int64_t cb0 = b * spc, cb1 = min(C, cb0 + spc);
+    const int tid = threadIdx.x;
+    if (cb0 >= C) return;
+    const uint32_t s0 = ws.cursor[row * RK_SB + b];
+    const uint32_t s1 = (b + 1 < RK_SB) ? ws.cursor[row * RK_SB + b + 1] : (uint32_t)K;
+    const int64_t nc = cb1 - cb0;
+    const bool in_lds = s1 - s0 <= (uint32_t)RK_FT;
+    for (int64_t c = tid; c < nc; c += RK_FTHR) fc[c] = 0;
+    __syncthreads();
+    uint32_t* idx = ws.ent_idx + row * ws.cap;
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(ws.ent_val + row * ws.cap);
+    constexpr int Q = RK_FT / RK_FTHR;
+    uint32_t jj[Q], rnk[Q];
+    if (in_lds) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t t = s0 + tid + q * RK_FTHR;
+            if (t < s1) {
+                jj[q] = idx[t];
+                rnk[q] = atomicAdd(&fc[(jj[q] >> CHUNK_SHIFT) - cb0], 1u);
+            }
+        }
+    } else {
+        for (uint32_t t = s0 + tid; t < s1; t += RK_FTHR) {
+            const uint32_t j = idx[t];
+            tmp[t] = j;
+            atomicAdd(&fc[(j >> CHUNK_SHIFT) - cb0], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of nc counters: thread t owns a contiguous block
+    const int64_t per = (nc + RK_FTHR - 1) / RK_FTHR;
+    const int64_t q0 = min<int64_t>(nc, tid * per), q1 = min<int64_t>(nc, q0 + per);
+    uint32_t loc = 0;
+    for (int64_t c = q0; c < q1; ++c) loc += fc[c];
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, WAVE);
+        if ((tid & 63) >= o) incl += u;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t run = incl - loc;
+    for (int w = 0; w < (tid >> 6); ++w) run += wsum[w];
+    for (int64_t c = q0; c < q1; ++c) {
+        const uint32_t v = fc[c];
+        ws.tab[(cb0 + c) * n + row] = make_uint2(s0 + run, v);
+        fc[c] = run;                                        // segment-relative offset
+        run += v;
+    }
+    __syncthreads();
+    const float* r = rows.row(row);
+    float* val = ws.ent_val + row * ws.cap;
+    if (in_lds) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t t = s0 + tid + q * RK_FTHR;
+            if (t < s1) tile[fc[(jj[q] >> CHUNK_SHIFT) - cb0] + rnk[q]] = jj[q];
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < s1 - s0; k += RK_FTHR) {
+            const uint32_t j = tile[k];
+            idx[s0 + k] = j;
+            val[s0 + k] = scale * r[j];                     // (D/K) * x[S] in fp32, ascending columns
+        }
+        return;
+    }
+    for (uint32_t t = s0 + tid; t < s1; t += RK_FTHR) {
+        const uint32_t j = tmp[t];
+        idx[s0 + atomicAdd(&fc[(j >> CHUNK_SHIFT) - cb0], 1u)] = j;
+    }
+    __syncthreads();                                        // block-scope visibility of the idx writes
+    for (uint32_t t = s0 + tid; t < s1; t += RK_FTHR) val[t] = scale * r[idx[t]];
+}
+
+// gather (D/K) * x[S] in fp32 in list order: chunk by chunk, so a wave's 64 reads fall in one or two
+// 16 KB windows of the row (HBM page locality) instead of the permutation's random order
+__global__ __launch_bounds__(256) void k_randk_gather(RowSrc rows, int64_t K, float scale, SelWs ws) {
+    const int64_t row = blockIdx.y;
+    const float* r = rows.row(row);
+    const uint32_t* idx = ws.ent_idx + row * ws.cap;
+    float* val = ws.ent_val + row * ws.cap;
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256)
+        val[t] = scale * r[idx[t]];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -927,7 +1181,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tieprefix = nullptr;
         s.tiecut = nullptr;
         s.hist = nullptr;
-        s.cursor = cv.take<uint32_t>((size_t)C * nn);
+        s.cursor = cv.take<uint32_t>((size_t)std::max<int64_t>(C, RK_SB) * nn);   // RandK: [N][RK_SB] segment offsets
     }
     if (bytes) *bytes = cv.bytes();
     return s;
@@ -977,15 +1231,36 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (codec == FLC_RANDK) {
         const int64_t ldi = (pat && pat->idx_ld) ? pat->idx_ld : K;
         flc_pattern p = pat ? *pat : flc_pattern{};
-        FLC_CHECK_HIP(hipMemsetAsync(ws.cursor, 0, (size_t)C * n * sizeof(uint32_t), st));
         dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>((K + 255) / 256, 64)), (unsigned)n);
-        hipLaunchKernelGGL(k_randk_count, g, dim3(256), 0, st, n, d, K, p, ldi, prm->seed, ws);
-        FLC_CHECK_LAUNCH("k_randk_count");
-        hipLaunchKernelGGL(k_randk_scan, dim3((unsigned)n), dim3(64), 0, st, n, d, ws);
-        FLC_CHECK_LAUNCH("k_randk_scan");
-        { ProfScope _ps("k_randk_scatter", st);
-hipLaunchKernelGGL(k_randk_scatter, g, dim3(256), 0, st, rows, n, d, K, p, ldi, prm->seed, prm->randk_scale, ws); }
-        FLC_CHECK_LAUNCH("k_randk_scatter");
+        if (!getenv("FLC_RANDK_GLOBAL")) {
+            const int64_t spc = rk_spc(C), sb = (C + spc - 1) / spc;
+            { ProfScope _ps("k_randk_coarse", st);
+            if (spc == 1)
+                hipLaunchKernelGGL(k_randk_coarse<true>, dim3((unsigned)n), dim3(RK_T), 0, st, rows, n, d, K, p, ldi,
+                                   prm->seed, prm->randk_scale, ws);
+            else
+                hipLaunchKernelGGL(k_randk_coarse<false>, dim3((unsigned)n), dim3(RK_T), 0, st, rows, n, d, K, p, ldi,
+                                   prm->seed, prm->randk_scale, ws); }
+            FLC_CHECK_LAUNCH("k_randk_coarse");
+            if (spc > 1) {
+                ProfScope _ps("k_randk_fine", st);
+                hipLaunchKernelGGL(k_randk_fine, dim3((unsigned)sb, (unsigned)n), dim3(RK_FTHR), (size_t)spc * sizeof(uint32_t),
+                                   st, rows, n, d, K, prm->randk_scale, ws);
+                FLC_CHECK_LAUNCH("k_randk_fine");
+            }
+        } else {
+            FLC_CHECK_HIP(hipMemsetAsync(ws.cursor, 0, (size_t)C * n * sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_randk_count, g, dim3(256), 0, st, n, d, K, p, ldi, prm->seed, ws);
+            FLC_CHECK_LAUNCH("k_randk_count");
+            hipLaunchKernelGGL(k_randk_scan, dim3((unsigned)n), dim3(64), 0, st, n, d, ws);
+            FLC_CHECK_LAUNCH("k_randk_scan");
+            { ProfScope _ps("k_randk_scatter", st);
+            hipLaunchKernelGGL(k_randk_scatter, g, dim3(256), 0, st, n, d, K, p, ldi, prm->seed, ws); }
+            FLC_CHECK_LAUNCH("k_randk_scatter");
+            { ProfScope _ps("k_randk_gather", st);
+            hipLaunchKernelGGL(k_randk_gather, g, dim3(256), 0, st, rows, K, prm->randk_scale, ws); }
+            FLC_CHECK_LAUNCH("k_randk_gather");
+        }
     } else {  // TOPK
         FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const bool dense_k = K * 16 > d;   // large K: the candidate list would not be smaller than the row

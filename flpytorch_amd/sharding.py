@@ -58,7 +58,9 @@ class ShardedUplink:
                 out.copy_(parts[0])
                 for p in parts[1:]:
                     out.add_(p)
-        out.div_(float(total_weight))
+        # a device-tensor divisor: torch turns a Python-scalar division on the GPU into a multiply
+        # by the reciprocal; the fold's contract (and the reference CPU path) is a true fp32 division
+        out.div_(torch.tensor(float(total_weight), dtype=torch.float32, device=out.device))
         return out
 
 

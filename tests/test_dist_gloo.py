@@ -103,3 +103,74 @@ def test_client_blocks_partition(n, world):
         assert 0 <= lo <= hi <= n
         seen.extend(range(lo, hi))
     assert seen == list(range(n))
+
+
+MIXED_SPECS = ["topk:5%", "ident", "topk:1"]
+
+
+def _mixed_oracle_partial(d):
+    def run(g, rows_g, c0, out):
+        acc = None
+        for r in rows_g:
+            e = oc.OracleCompressor(MIXED_SPECS[g], d).compress(r.numpy())
+            acc = e.copy() if acc is None else acc + e
+        out.copy_(torch.from_numpy(acc))
+    return run
+
+
+def _mixed_worker(rank, world, port, n, d, q):
+    from flpytorch_amd.aggregation.mixed import MixedUplink
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = make_rows(n, d)
+    per = n // world
+    lo = rank * per
+    up = MixedUplink(MIXED_SPECS, d, seed=1, encode_partial=_mixed_oracle_partial(d))
+    out = up(torch.from_numpy(rows[lo:lo + per].copy()), client0=lo, group=dist.group.WORLD)
+    q.put((rank, out.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_mixed_uplink_two_ranks():
+    """C5's combine: per-codec-group partials, each all-reduced asynchronously, summed in group
+    order, divided by the global client count — equal on both ranks and to the stated order."""
+    world, n, d = 2, 12, 2053
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mixed_worker, args=(r, world, port, n, d, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rows = make_rows(n, d)
+    G = len(MIXED_SPECS)
+    per = n // world
+    parts = []
+    for g in range(G):
+        rank_sums = []
+        for r in range(world):
+            acc = None
+            for i in range(r * per + g, (r + 1) * per, G):        # global client i uses codec i mod G
+                e = oc.OracleCompressor(MIXED_SPECS[g], d).compress(rows[i])
+                acc = e.copy() if acc is None else acc + e
+            rank_sums.append(acc)
+        parts.append(rank_sums[0] + rank_sums[1])
+    want = parts[0].copy()
+    for p in parts[1:]:
+        want = want + p
+    want = want / np.float32(n)
+    np.testing.assert_array_equal(res[0], res[1])
+    np.testing.assert_array_equal(res[0], want)
+
+
+def test_mixed_uplink_groups():
+    from flpytorch_amd.aggregation.mixed import MixedUplink
+    up = MixedUplink(["a", "b", "c"], 10, seed=0, encode_partial=lambda *a: None)
+    assert up.groups(6, 7) == [([0, 3, 6], 2), ([1, 4], 2), ([2, 5], 2)]
+    with pytest.raises(ValueError):
+        up.groups(4, 3)
+    assert len(set(up.seeds)) == 3

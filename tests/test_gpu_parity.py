@@ -318,3 +318,36 @@ def test_fast_division_selftest(ag):
     _lib.check(lib.flc_selftest_division(b.data_ptr(), len(bs), bad.data_ptr(), _lib.stream_ptr()), "selftest")
     torch.cuda.synchronize()
     assert bad.cpu().tolist() == [0] * len(bs)
+
+
+@pytest.mark.parametrize("mode", ["compat", "device", "skewed"])
+@pytest.mark.parametrize("d,k", [(5_000_003, 50_001), (2_500_000, 20_000)])
+def test_randk_large_rows(ag, mode, d, k):
+    """RandK beyond one chunk per superchunk (D > 1 M: coarse + fine bucketing); 'skewed' compat
+    lists put every index in the first superchunk (the fine kernel's in-memory path)."""
+    from flpytorch_amd import _lib
+    lib = _lib.load()
+    n, seed, client0 = 3, 31337, 5
+    g = np.random.default_rng([d, k])
+    rows = g.standard_normal((n, d)).astype(np.float32)
+    idx = []
+    for i in range(n):
+        if mode == "device":
+            s = np.empty(k, dtype=np.int64)
+            assert lib.flc_device_randk_indices(seed, client0 + i, d, k, s.ctypes.data) == 0
+            assert np.unique(s).size == k and s.min() >= 0 and s.max() < d
+        elif mode == "skewed":
+            s = g.permutation(k + 7)[:k].astype(np.int64)        # all inside [0, k + 7)
+        else:
+            s = g.choice(d, k, replace=False).astype(np.int64)
+        idx.append(s)
+    enc = []
+    for i in range(n):
+        o = oc.OracleCompressor(f"randk:{k}", d)
+        o.S = idx[i]
+        enc.append(o.compress(rows[i]))
+    want = oc.reduce_plain(enc)
+    red = ag.UplinkReducer(ag.initCompressor(f"randk:{k}", d), seed=seed)
+    kw = {} if mode == "device" else {"randk_idx": torch.from_numpy(np.stack(idx)).cuda()}
+    got = red(torch.from_numpy(rows).cuda(), client0=client0, **kw)
+    assert_bitexact(got, want)
