@@ -191,3 +191,24 @@ def test_algorithm_steps(ag, spec):
     mult = 1.0 if c0.isContractionCompressor() else 1.0 / (1.0 + c0.getW())
     assert_bitexact(ag.ef21Step(comp(), grad, gp), gp + comp().compressVector(grad - gp) * mult)
     assert_bitexact(ag.marinaStep(comp(), grad, gpx, gp), gp + comp().compressVector(grad - gpx))
+
+
+def test_arena_views_feed_the_kernels(ag):
+    """A model's gradient arena (flpytorch_amd.arena) is read in place by the codecs: the EF21 step
+    on grad_view() equals the step on mutils-style concatenated copies."""
+    from flpytorch_amd.arena import FlatArena
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 10)).cuda()
+    a = FlatArena(m)
+    x = torch.randn(32, 64, device="cuda")
+    m(x).square().mean().backward()
+    g = a.grad_view()
+    cat = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    assert g.data_ptr() == a.gflat.data_ptr() and torch.equal(g, cat)
+    gp = torch.randn_like(g)
+
+    def comp():
+        c = ag.initCompressor("qsgd:8", a.D)
+        c.generateCompressPattern(np.random.RandomState(1), "cuda", 0, {})
+        return c
+    assert_bitexact(ag.ef21Step(comp(), g, gp), ag.ef21Step(comp(), cat, gp))
