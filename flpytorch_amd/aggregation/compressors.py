@@ -360,6 +360,64 @@ class Compressor:
         out = out.reshape(x.shape)
         return out.to("cpu") if host_in else out
 
+    # -- wire format ------------------------------------------------------
+    def payloadBytes(self, d=None):
+        """Bytes of one row's payload (flc_payload_bytes: 16-B header + body, 16-B padded)."""
+        prm, _ = self.codec_params(torch.device("cpu")) if self.compressorType not in (
+            CompressorType.STANDARD_DITHERING_FP32, CompressorType.NATURAL_DITHERING_FP32) else (None, None)
+        if prm is None:
+            prm = _lib.FlcCodecParams()
+            prm.codec = int(self.compressorType)
+            prm.s = int(self.s)
+        return int(_lib.load().flc_payload_bytes(ctypes.byref(prm), self._dim(d)))
+
+    def _dim(self, d):
+        if d is None:
+            d = getattr(self, "D", None)
+        if d is None:
+            raise ValueError("this compressor has no D (identity): pass d")
+        return int(d)
+
+    def compressPayload(self, x, out=None):
+        """The message this client would send: flc_pack of compressVector(x) (same pattern, same
+        draws), as a uint8 device tensor of payloadBytes() bytes.  Statistics advance like
+        compressVector."""
+        if x.dtype != torch.float32:
+            raise TypeError(f"flcodec encodes fp32 only (got {x.dtype})")
+        dev = _gpu_device(x)
+        xd = x.reshape(-1).to(device=dev).contiguous()
+        d = xd.numel()
+        lib = _lib.load()
+        prm, keep = self.codec_params(dev)
+        pat = self._pattern(dev, keep)
+        nbytes = int(lib.flc_payload_bytes(ctypes.byref(prm), d))
+        if out is None:
+            out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        elif out.numel() < nbytes or out.dtype != torch.uint8 or out.data_ptr() % 16:
+            raise ValueError("compressPayload: out must be a 16-byte aligned uint8 tensor of payloadBytes()")
+        ws_bytes = lib.flc_pack_workspace_size(ctypes.byref(prm), d)
+        ws = _lib.WORKSPACE.get(dev, ws_bytes)
+        with torch.cuda.device(dev):
+            rc = lib.flc_pack(ctypes.byref(prm), ctypes.byref(pat), ctypes.c_void_p(xd.data_ptr()), d,
+                              ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                              _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_pack")
+        self._account(d)
+        return out
+
+    def decompressPayload(self, payload, d=None):
+        """Dense fp32 row of a payload (flc_unpack): compressVector's output, bit for bit."""
+        dev = _gpu_device(payload)
+        d = self._dim(d)
+        lib = _lib.load()
+        prm, keep = self.codec_params(dev)
+        out = torch.empty(d, dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.flc_unpack(ctypes.byref(prm), ctypes.c_void_p(payload.data_ptr()), d,
+                                ctypes.c_void_p(out.data_ptr()), _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_unpack")
+        return out
+
     # -- shift codecs (SURVEY §8f rank 1) ----------------------------------------------------
     def compressShift(self, a, b, *, scale=1.0, base=None, out=None, alpha=None, shift=None, shift_out=None,
                       message=True, pnorm_out=None):

@@ -109,3 +109,58 @@ class UplinkReducer:
                                        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(), st)
         _lib.check(rc, "flc_encode_reduce")
         return out
+
+
+class PayloadReducer:
+    """Server side of the wire format: out = (sum_i w_i * decode(payload_i)) / sum(w), folded in
+    client order straight from the messages (flc_unpack_reduce) — the same bits as
+    flc_encode_reduce of the rows the payloads were packed from."""
+
+    def __init__(self, compressor: Compressor, device=None):
+        _lib.require_gpu()
+        self.comp = compressor
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+    def __call__(self, payloads, d=None, out=None, weights=None, divisor=None):
+        """payloads: [N, ld] uint8 device tensor (rows 16-byte aligned, ld % 16 == 0) or a list of
+        uint8 device tensors."""
+        lib = _lib.load()
+        dev = self.device
+        d = self.comp._dim(d)
+        prm, keep = self.comp.codec_params(dev)
+        if torch.is_tensor(payloads) and payloads.dim() == 2:
+            n, ld = payloads.shape
+            if payloads.stride(1) != 1 or payloads.stride(0) % 16 or payloads.data_ptr() % 16:
+                raise ValueError("payload rows must be contiguous and 16-byte aligned")
+            base, ldb, ptrs = payloads.data_ptr(), payloads.stride(0), None
+        else:
+            n = len(payloads)
+            for p in payloads:
+                if p.data_ptr() % 16:
+                    raise ValueError("payloads must be 16-byte aligned")
+            host_pt = torch.tensor([p.data_ptr() for p in payloads], dtype=torch.int64).pin_memory()
+            pt = host_pt.to(dev, non_blocking=True)
+            keep.extend(payloads)
+            keep.append(pt)
+            base, ldb, ptrs = None, 0, pt.data_ptr()
+        if out is None:
+            out = torch.empty(d, dtype=torch.float32, device=dev)
+        w_ptr, total = None, float(n)
+        if weights is not None:
+            weights = [float(w) for w in weights]
+            total = weights[0]
+            for w in weights[1:]:
+                total += w
+            wt = torch.tensor(weights, dtype=torch.float32, device=dev)
+            keep.append(wt)
+            w_ptr = wt.data_ptr()
+        if divisor is not None:
+            total = float(divisor)
+        ws_bytes = lib.flc_unpack_reduce_workspace_size(ctypes.byref(prm), n, d)
+        ws = _lib.WORKSPACE.get(dev, ws_bytes)
+        with torch.cuda.device(dev):
+            rc = lib.flc_unpack_reduce(ctypes.byref(prm), ctypes.c_void_p(base), ldb, ctypes.c_void_p(ptrs), n, d,
+                                       ctypes.c_void_p(w_ptr), ctypes.c_float(total), ctypes.c_void_p(out.data_ptr()),
+                                       ctypes.c_void_p(ws.data_ptr()), ws.numel(), _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_unpack_reduce")
+        return out

@@ -108,6 +108,15 @@ extern "C" int flc_selftest_division(const float* d_divisors, int n, unsigned lo
     return selftest_division(d_divisors, n, d_mismatches, (hipStream_t)stream);
 }
 
+namespace flc {
+size_t encode_row_workspace(const flc_codec_params* prm, int64_t d) {
+    if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
+    if (prm->codec == FLC_RANK_K) return rk_workspace(prm, 1, d, false);
+    if (prm->codec == FLC_RANDK) return 0;
+    return ew_workspace(prm, 1, d);
+}
+}  // namespace flc
+
 extern "C" size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t d) {
     if (!prm || !known(prm->codec)) return 0;
     if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
@@ -123,12 +132,10 @@ extern "C" size_t flc_encode_reduce_workspace_size(const flc_codec_params* prm, 
     return ew_workspace(prm, n, d);
 }
 
-extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
-                          const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes,
-                          void* stream) {
-    if (!prm || !known(prm->codec)) { set_error("flc_encode: unknown codec"); return FLC_ERR_UNSUPPORTED; }
-    if (d < 0 || (d > 0 && (!d_x || !d_out))) { set_error("flc_encode: bad x/out/d"); return FLC_ERR_ARG; }
-    hipStream_t st = (hipStream_t)stream;
+namespace flc {
+// one row, dense output (flc_encode; also the first stage of flc_pack)
+int encode_row(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+               const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes, hipStream_t st) {
     const bool vec = (((uintptr_t)d_x | (uintptr_t)d_out) & 15u) == 0;
     switch (prm->codec) {
         case FLC_RANDK:
@@ -149,6 +156,15 @@ extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, c
         }
     }
 }
+}  // namespace flc
+
+extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+                          const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes,
+                          void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_encode: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (d < 0 || (d > 0 && (!d_x || !d_out))) { set_error("flc_encode: bad x/out/d"); return FLC_ERR_ARG; }
+    return encode_row(prm, pat, d_x, d, d_pnorm_in, d_pnorm_out, d_out, d_ws, ws_bytes, (hipStream_t)stream);
+}
 
 extern "C" size_t flc_encode_shift_workspace_size(const flc_codec_params* prm, int64_t d) {
     if (!prm || !known(prm->codec) || d < 0) return 0;
@@ -167,6 +183,50 @@ extern "C" int flc_encode_shift(const flc_codec_params* prm, const flc_pattern* 
     if (d_base && !d_msg) { set_error("flc_encode_shift: base without msg"); return FLC_ERR_ARG; }
     ShiftArgs sh{d_b, msg_scale, d_base, d_msg, shift_alpha, d_shift_in, d_shift_out};
     return shift_run(prm, pat, d_a, d, sh, d_pnorm_out, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int64_t flc_payload_bytes(const flc_codec_params* prm, int64_t d) {
+    if (!prm || !known(prm->codec) || d < 0) return 0;
+    return payload_bytes(prm, d);
+}
+
+extern "C" int flc_payload_format(const flc_codec_params* prm) {
+    if (!prm || !known(prm->codec)) return 0;
+    return payload_format(prm);
+}
+
+extern "C" size_t flc_pack_workspace_size(const flc_codec_params* prm, int64_t d) {
+    if (!prm || !known(prm->codec) || d < 0) return 0;
+    return pack_workspace(prm, d);
+}
+
+extern "C" int flc_pack(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+                        void* d_payload, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_pack: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (d < 0 || !d_payload || (d > 0 && !d_x)) { set_error("flc_pack: bad x/payload/d"); return FLC_ERR_ARG; }
+    return pack_run(prm, pat, d_x, d, (char*)d_payload, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int flc_unpack(const flc_codec_params* prm, const void* d_payload, int64_t d, float* d_out, void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_unpack: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (d < 0 || (d > 0 && (!d_payload || !d_out))) { set_error("flc_unpack: bad payload/out/d"); return FLC_ERR_ARG; }
+    return unpack_run(prm, (const char*)d_payload, d, d_out, (hipStream_t)stream);
+}
+
+extern "C" size_t flc_unpack_reduce_workspace_size(const flc_codec_params* prm, int64_t n, int64_t d) {
+    if (!prm || !known(prm->codec) || n < 0 || d < 0) return 0;
+    return unpack_reduce_workspace(prm, n, d);
+}
+
+extern "C" int flc_unpack_reduce(const flc_codec_params* prm, const void* d_payloads, int64_t ld_bytes,
+                                 const void* const* d_payload_ptrs, int64_t n, int64_t d, const float* d_w,
+                                 float w_total, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!prm || !known(prm->codec)) { set_error("flc_unpack_reduce: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (n < 0 || d < 0 || (d > 0 && !d_out)) { set_error("flc_unpack_reduce: bad n/d/out"); return FLC_ERR_ARG; }
+    if (n > 0 && d > 0 && !d_payloads && !d_payload_ptrs) { set_error("flc_unpack_reduce: no payloads"); return FLC_ERR_ARG; }
+    if (d_payloads && ld_bytes < payload_bytes(prm, d)) { set_error("flc_unpack_reduce: ld_bytes < payload size"); return FLC_ERR_ARG; }
+    return unpack_reduce_run(prm, (const char*)d_payloads, ld_bytes, (const char* const*)d_payload_ptrs, n, d, d_w,
+                             w_total, d_out, d_ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern* pat, const float* d_rows, int64_t ld,

@@ -96,6 +96,22 @@ int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool
            const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt, void* ws,
            size_t ws_bytes, hipStream_t st, const ShiftArgs* sh = nullptr);
 size_t shift_workspace(const flc_codec_params* prm, int64_t d);
+int encode_row(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+               const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes, hipStream_t st);
+size_t encode_row_workspace(const flc_codec_params* prm, int64_t d);
+int sel_unpack_reduce(const flc_codec_params* prm, const void* base, int64_t ld_bytes, const void* const* ptrs,
+                      int64_t n, int64_t d, const float* w, float wt, float* out, void* wsp, size_t ws_bytes,
+                      hipStream_t st);
+size_t sel_unpack_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+int64_t payload_bytes(const flc_codec_params* prm, int64_t d);
+int payload_format(const flc_codec_params* prm);
+size_t pack_workspace(const flc_codec_params* prm, int64_t d);
+int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, char* payload, void* ws,
+             size_t ws_bytes, hipStream_t st);
+int unpack_run(const flc_codec_params* prm, const char* payload, int64_t d, float* out, hipStream_t st);
+size_t unpack_reduce_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+int unpack_reduce_run(const flc_codec_params* prm, const char* base, int64_t ld, const char* const* ptrs, int64_t n,
+                      int64_t d, const float* w, float wt, float* out, void* ws, size_t ws_bytes, hipStream_t st);
 int shift_run(const flc_codec_params* prm, const flc_pattern* pat, const float* a, int64_t d, const ShiftArgs& sh,
               float* pnorm_out, void* ws, size_t ws_bytes, hipStream_t st);
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);

@@ -1312,6 +1312,76 @@ if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st
     return FLC_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// Decode + reduce of sparse wire payloads (wire.hip, SPARSE: 16-B header {fmt, count, norm, bad},
+// u32 idx[cap], f32 val[cap], ascending idx): the entries are copied into the selection lists,
+// each (chunk, row) range is found by binary search, and k_chunk_accum folds them in row order —
+// the same fold as flc_encode_reduce, so the result is the same bits.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_unpack_lists(const char* __restrict__ base, int64_t ld,
+                                                      const char* const* __restrict__ ptrs, int64_t n, int64_t cap,
+                                                      int64_t pcap, SelWs ws) {
+    const int64_t row = blockIdx.y;
+    const char* p = base ? base + row * ld : ptrs[row];
+    const uint32_t cnt = (uint32_t)min<int64_t>(reinterpret_cast<const uint32_t*>(p)[1], min(cap, pcap));
+    const uint32_t* pi = reinterpret_cast<const uint32_t*>(p + 16);
+    const float* pv = reinterpret_cast<const float*>(p + 16 + ((4 * pcap + 15) & ~int64_t(15)));
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * 256) {
+        ws.ent_idx[row * ws.cap + e] = pi[e];
+        ws.ent_val[row * ws.cap + e] = pv[e];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ws.thr[row] = 0;
+        ws.flags[row] = F_EXACT;
+        ws.rowcnt[row * RCS] = cnt;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_tab(int64_t n, int64_t d, SelWs ws) {
+    const int64_t row = blockIdx.y, C = nchunks(d);
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const uint32_t cnt = ws.rowcnt[row * RCS];
+    const uint32_t* idx = ws.ent_idx + row * ws.cap;
+    auto lb = [&](uint64_t key) {
+        uint32_t lo = 0, hi = cnt;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint64_t)idx[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    };
+    const uint32_t a = lb((uint64_t)c << CHUNK_SHIFT), b = lb((uint64_t)(c + 1) << CHUNK_SHIFT);
+    ws.tab[c * n + row] = make_uint2(a, b - a);
+}
+
+size_t sel_unpack_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
+    size_t b = 0;
+    carve_sel(nullptr, FLC_RANDK, n, d, std::max<int64_t>(1, std::min(prm->k, d)), &b);
+    return b;
+}
+
+int sel_unpack_reduce(const flc_codec_params* prm, const void* base, int64_t ld_bytes, const void* const* ptrs,
+                      int64_t n, int64_t d, const float* w, float wt, float* out, void* wsp, size_t ws_bytes,
+                      hipStream_t st) {
+    const int64_t K = std::max<int64_t>(1, std::min(prm->k, d));
+    if (ws_bytes < sel_unpack_workspace(prm, n, d)) { set_error("flc_unpack_reduce: workspace too small"); return FLC_ERR_WORKSPACE; }
+    if (d >= (int64_t)0xFFFFFFFF) { set_error("D too large for 32-bit entry indices"); return FLC_ERR_ARG; }
+    SelWs ws = carve_sel(wsp, FLC_RANDK, n, d, K, nullptr);
+    const int64_t C = host_chunks(d);
+    dim3 g1((unsigned)std::max<int64_t>(1, std::min<int64_t>((K + 255) / 256, 64)), (unsigned)n);
+    hipLaunchKernelGGL(k_unpack_lists, g1, dim3(256), 0, st, (const char*)base, ld_bytes, (const char* const*)ptrs, n,
+                       ws.cap, K, ws);
+    FLC_CHECK_LAUNCH("k_unpack_lists");
+    hipLaunchKernelGGL(k_unpack_tab, dim3((unsigned)((C + 255) / 256), (unsigned)n), dim3(256), 0, st, n, d, ws);
+    FLC_CHECK_LAUNCH("k_unpack_tab");
+    const int ab = grid_stride_blocks((C + 3) / 4, 4096);
+    { ProfScope _ps("k_chunk_accum", st);
+    hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out); }
+    FLC_CHECK_LAUNCH("k_chunk_accum");
+    return FLC_OK;
+}
+
 // Dense single-vector RandK: out = 0; out[S] = scale * x[S]  (compressors.py:242-243)
 __global__ __launch_bounds__(256) void k_randk_dense(const float* __restrict__ x, int64_t d, int64_t K, flc_pattern pat,
                                                      uint64_t seed, float scale, float* __restrict__ out) {

@@ -1,0 +1,390 @@
+// Wire format: the compressed message a client would actually send, and the
+// server's decode + reduce straight from the N messages (fl_pytorch/utils/compressors.py:223-224,
+// 367-368 count these bits as last_need_to_send_advance, but the reference only ever moves the
+// dense decoded tensor; comm_socket.py pickles that).
+//
+// One row's payload: a 16-B header {u32 format, u32 count, f32 norm, u32 d} and a body, 16-B padded:
+//   F32     ident / lazy / natural dithering (the reference's output is ~x) / rank_k: f32[d]
+//   Q8      standard dithering / QSGD / TernGrad, s <= 127: u8[d]   bit 7 sign, bits 0-6 level index
+//   Q16     standard dithering, 127 < s <= 32767:         u16[d]  bit 15 sign, bits 0-14 level index
+//   NAT16   natural:                                       u16[d]  bit 15 sign, bits 0-14: 0 zero,
+//           0x7FFE inf, 0x7FFF NaN, else k + 16384 for the value 2^k (k in [-149, 127])
+//   SPARSE  randk / topk: count (<= K) entries, u32 idx[K] then f32 val[K], ascending idx; the
+//           entries are the output's elements whose bits are not +0
+// Level codes: value = (levels[idx] * sign) * norm exactly as the encode (compressors.py:294-296);
+// code 0 is +0 exactly (x == 0), sign + level 0 with the sign bit is -0 * norm (NaN when the norm is
+// not finite).  Decoding a payload gives the dense compressVector output bit for bit
+// (flc_pack -> flc_unpack), and flc_unpack_reduce equals flc_encode_reduce of the same rows.
+//
+// flc_pack runs the row's ordinary encode into the workspace first (so every draw, norm and tie
+// rule is the encode's) and derives the codes from the dense output: a level index is the one whose
+// (levels[i] * sign) * norm reproduces the element's bits (guess rint(y s), then its neighbours,
+// then a binary search); elements no level reproduces are counted in the header's `bad` field
+// (never seen: the encode's outputs are of that form by construction; the tests assert 0).
+#include "common.hpp"
+
+namespace flc {
+
+enum { FMT_F32 = 1, FMT_Q8 = 2, FMT_Q16 = 3, FMT_NAT16 = 4, FMT_SPARSE = 5 };
+struct PayloadHeader {
+    uint32_t fmt, count;
+    float norm;
+    uint32_t bad;          // elements whose code search failed (0 by construction)
+};
+
+__host__ __device__ inline int64_t a16(int64_t b) { return (b + 15) & ~int64_t(15); }
+
+int payload_format(const flc_codec_params* prm) {
+    switch (prm->codec) {
+        case FLC_STD_DITHERING: return prm->s <= 127 ? FMT_Q8 : FMT_Q16;
+        case FLC_NATURAL: return FMT_NAT16;
+        case FLC_RANDK:
+        case FLC_TOPK: return FMT_SPARSE;
+        default: return FMT_F32;
+    }
+}
+
+int64_t payload_bytes(const flc_codec_params* prm, int64_t d) {
+    switch (payload_format(prm)) {
+        case FMT_Q8: return 16 + a16(d);
+        case FMT_Q16:
+        case FMT_NAT16: return 16 + a16(2 * d);
+        case FMT_SPARSE: { const int64_t k = std::max<int64_t>(1, std::min(prm->k, d)); return 16 + 2 * a16(4 * k); }
+        default: return 16 + a16(4 * d);
+    }
+}
+
+// ---- level codes ------------------------------------------------------------------------------
+__device__ inline float lev_value(const float* lv, uint32_t idx, bool neg, float norm) {
+    return copysignf(lv[idx], neg ? -1.f : 1.f) * norm;
+}
+
+__device__ inline uint32_t lev_code(float v, const float* lv, int s, float norm, uint32_t sbit, uint32_t* bad) {
+    const uint32_t vb = __float_as_uint(v);
+    if (vb == 0u) return 0u;                                   // +0 (x == 0)
+    const bool neg = (vb >> 31) != 0u;
+    if (v != v) return sbit;                                   // NaN: -0 * non-finite norm
+    const float y = fabsf(v) / norm;
+    int g = (int)rintf(y * (float)s);
+    g = g < 0 ? 0 : (g > s ? s : g);
+    for (int dlt = 0; dlt < 3; ++dlt) {
+        const int c = dlt == 0 ? g : (dlt == 1 ? g - 1 : g + 1);
+        if (c >= 0 && c <= s && __float_as_uint(lev_value(lv, (uint32_t)c, neg, norm)) == vb)
+            return (neg ? sbit : 0u) | (uint32_t)c;
+    }
+    int lo = 0, hi = s;                                        // levels ascending: binary search on |v|
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const float m = fabsf(lev_value(lv, (uint32_t)mid, neg, norm));
+        if (__float_as_uint(lev_value(lv, (uint32_t)mid, neg, norm)) == vb) return (neg ? sbit : 0u) | (uint32_t)mid;
+        if (m < fabsf(v)) lo = mid + 1; else hi = mid - 1;
+    }
+    atomicAdd(bad, 1u);
+    return neg ? sbit : 0u;
+}
+
+__device__ inline float lev_decode(uint32_t code, const float* lv, float norm, uint32_t sbit) {
+    if (code == 0u) return 0.f;
+    return lev_value(lv, code & (sbit - 1u), (code & sbit) != 0u, norm);
+}
+
+// ---- natural codes ----------------------------------------------------------------------------
+__device__ inline uint32_t nat_code(float v) {
+    const uint32_t vb = __float_as_uint(v), sg = (vb >> 31) << 15;
+    if ((vb & 0x7FFFFFFFu) == 0u) return sg;
+    if (v != v) return 0x7FFFu;
+    if (isinf(v)) return sg | 0x7FFEu;
+    int e;
+    (void)frexpf(v, &e);                                       // |v| = 0.5 * 2^e (a power of two)
+    return sg | (uint32_t)(e - 1 + 16384);
+}
+
+__device__ inline float nat_decode(uint32_t c) {
+    const float sg = (c & 0x8000u) ? -1.f : 1.f;
+    const uint32_t m = c & 0x7FFFu;
+    if (m == 0u) return copysignf(0.f, sg);
+    if (m == 0x7FFFu) return __uint_as_float(0x7FC00000u);
+    if (m == 0x7FFEu) return copysignf(__builtin_inff(), sg);
+    return copysignf(ldexpf(1.f, (int)m - 16384), sg);
+}
+
+// ---- pack ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack_dense(const float* __restrict__ v, int64_t d, int fmt,
+                                                    const float* __restrict__ levels, int s,
+                                                    const float* __restrict__ pnorm, char* __restrict__ payload) {
+    PayloadHeader* h = reinterpret_cast<PayloadHeader*>(payload);
+    char* body = payload + 16;
+    const float norm = pnorm ? *pnorm : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        h->fmt = (uint32_t)fmt;
+        h->count = (uint32_t)d;
+        h->norm = norm;
+    }
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
+        const float x = v[j];
+        if (fmt == FMT_F32) reinterpret_cast<float*>(body)[j] = x;
+        else if (fmt == FMT_Q8) reinterpret_cast<uint8_t*>(body)[j] = (uint8_t)lev_code(x, levels, s, norm, 0x80u, &h->bad);
+        else if (fmt == FMT_Q16) reinterpret_cast<uint16_t*>(body)[j] = (uint16_t)lev_code(x, levels, s, norm, 0x8000u, &h->bad);
+        else reinterpret_cast<uint16_t*>(body)[j] = (uint16_t)nat_code(x);
+    }
+}
+
+constexpr int PK_BLK = 4096;   // elements per compaction block
+
+__global__ __launch_bounds__(256) void k_pack_count(const float* __restrict__ v, int64_t d, uint32_t* __restrict__ bc) {
+    const int64_t b = blockIdx.x, j0 = b * PK_BLK, j1 = min(d, j0 + PK_BLK);
+    uint32_t c = 0;
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) c += __float_as_uint(v[j]) != 0u;
+    c = wave_sum(c);
+    __shared__ uint32_t ws4[4];
+    if ((threadIdx.x & 63) == 0) ws4[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[b] = ws4[0] + ws4[1] + ws4[2] + ws4[3];
+}
+
+__global__ __launch_bounds__(1024) void k_pack_scan(uint32_t* __restrict__ bc, int64_t nb, char* __restrict__ payload,
+                                                    int64_t cap) {
+    __shared__ uint32_t wsum[16];
+    const int tid = threadIdx.x;
+    const int64_t per = (nb + 1023) / 1024, q0 = min<int64_t>(nb, tid * per), q1 = min<int64_t>(nb, q0 + per);
+    uint32_t loc = 0;
+    for (int64_t q = q0; q < q1; ++q) loc += bc[q];
+    uint32_t incl = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, WAVE);
+        if ((tid & 63) >= o) incl += u;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t run = incl - loc;
+    for (int w = 0; w < (tid >> 6); ++w) run += wsum[w];
+    for (int64_t q = q0; q < q1; ++q) { const uint32_t c = bc[q]; bc[q] = run; run += c; }
+    if (tid == 1023) {
+        PayloadHeader* h = reinterpret_cast<PayloadHeader*>(payload);
+        h->fmt = FMT_SPARSE;
+        h->count = run;
+        h->norm = 0.f;
+        h->bad = run > (uint64_t)cap ? run - (uint32_t)cap : 0u;   // more nonzeros than K: never for RandK / TopK
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pack_write(const float* __restrict__ v, int64_t d, const uint32_t* __restrict__ bc,
+                                                    char* __restrict__ payload, int64_t cap) {
+    const int64_t b = blockIdx.x, j0 = b * PK_BLK;
+    uint32_t* idx = reinterpret_cast<uint32_t*>(payload + 16);
+    float* val = reinterpret_cast<float*>(payload + 16 + a16(4 * cap));
+    __shared__ uint32_t wsum[4];
+    uint32_t base = bc[b];
+    for (int64_t s0 = j0; s0 < min(d, j0 + PK_BLK); s0 += 256) {
+        const int64_t j = s0 + threadIdx.x;
+        const float x = j < d ? v[j] : 0.f;
+        const bool keep = j < d && __float_as_uint(x) != 0u;
+        const uint64_t m = __ballot(keep);
+        const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) wsum[wv] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        uint32_t off = base;
+        for (uint32_t w = 0; w < wv; ++w) off += wsum[w];
+        if (keep && off + rank < (uint64_t)cap) { idx[off + rank] = (uint32_t)j; val[off + rank] = x; }
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
+
+// ---- unpack (one row) --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_unpack_dense(const char* __restrict__ payload, int64_t d,
+                                                      const float* __restrict__ levels, float* __restrict__ out) {
+    const PayloadHeader h = *reinterpret_cast<const PayloadHeader*>(payload);
+    const char* body = payload + 16;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
+        float x;
+        if (h.fmt == FMT_F32) x = reinterpret_cast<const float*>(body)[j];
+        else if (h.fmt == FMT_Q8) x = lev_decode(reinterpret_cast<const uint8_t*>(body)[j], levels, h.norm, 0x80u);
+        else if (h.fmt == FMT_Q16) x = lev_decode(reinterpret_cast<const uint16_t*>(body)[j], levels, h.norm, 0x8000u);
+        else x = nat_decode(reinterpret_cast<const uint16_t*>(body)[j]);
+        out[j] = x;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_sparse(const char* __restrict__ payload, int64_t cap, float* __restrict__ out) {
+    const PayloadHeader h = *reinterpret_cast<const PayloadHeader*>(payload);
+    const uint32_t* idx = reinterpret_cast<const uint32_t*>(payload + 16);
+    const float* val = reinterpret_cast<const float*>(payload + 16 + a16(4 * cap));
+    const int64_t cnt = min<int64_t>(h.count, cap);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * blockDim.x)
+        out[idx[e]] = val[e];
+}
+
+// ---- decode + reduce over n payloads (dense formats) --------------------------------------------
+// Tile owner: each thread owns 4 consecutive columns for the whole fold, rows in order, so the fp32
+// sum is the sequential one: acc = t_0; acc = acc + t_i; out = acc / wt  (t_i = w_i * dec_i).
+template <int FMT, bool W>
+__global__ __launch_bounds__(256) void k_unpack_accum(const char* __restrict__ base, int64_t ld,
+                                                      const char* const* __restrict__ ptrs, int64_t n, int64_t d,
+                                                      const float* __restrict__ levels, const float* __restrict__ w,
+                                                      float wt, float* __restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t j0 = g * 4;
+    if (j0 >= d) return;
+    const int m = (int)min<int64_t>(4, d - j0);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t i = 0; i < n; ++i) {
+        const char* p = base ? base + i * ld : sload(ptrs + i);
+        const float norm = (FMT == FMT_Q8 || FMT == FMT_Q16) ? sload(reinterpret_cast<const float*>(p + 8)) : 0.f;
+        const float wi = W ? w[i] : 1.f;
+        float e[4];
+        const char* body = p + 16;
+        if (FMT == FMT_Q8) {
+            uint32_t c4;
+            if (m == 4) c4 = *reinterpret_cast<const uint32_t*>(body + j0);
+            else { c4 = 0; for (int q = 0; q < m; ++q) c4 |= (uint32_t)reinterpret_cast<const uint8_t*>(body)[j0 + q] << (8 * q); }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) e[q] = lev_decode((c4 >> (8 * q)) & 0xFFu, levels, norm, 0x80u);
+        } else if (FMT == FMT_Q16 || FMT == FMT_NAT16) {
+            uint2 c2;
+            if (m == 4) c2 = *reinterpret_cast<const uint2*>(body + 2 * j0);
+            else {
+                uint32_t c[4] = {0, 0, 0, 0};
+                for (int q = 0; q < m; ++q) c[q] = reinterpret_cast<const uint16_t*>(body)[j0 + q];
+                c2 = make_uint2(c[0] | (c[1] << 16), c[2] | (c[3] << 16));
+            }
+            const uint32_t cc[4] = {c2.x & 0xFFFFu, c2.x >> 16, c2.y & 0xFFFFu, c2.y >> 16};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                e[q] = FMT == FMT_NAT16 ? nat_decode(cc[q]) : lev_decode(cc[q], levels, norm, 0x8000u);
+        } else {
+            float4 v;
+            if (m == 4) v = *reinterpret_cast<const float4*>(body + 4 * j0);
+            else {
+                float t[4] = {0.f, 0.f, 0.f, 0.f};
+                for (int q = 0; q < m; ++q) t[q] = reinterpret_cast<const float*>(body)[j0 + q];
+                v = make_float4(t[0], t[1], t[2], t[3]);
+            }
+            e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float t = W ? wi * e[q] : e[q];
+            acc[q] = (i == 0) ? t : acc[q] + t;
+        }
+    }
+    for (int q = 0; q < m; ++q) out[j0 + q] = acc[q] / wt;
+}
+
+// ---- host ----------------------------------------------------------------------------------------
+struct PackWs {
+    float* dense;
+    float* pnorm;
+    uint32_t* bc;
+    void* inner;
+    size_t inner_bytes;
+};
+static PackWs carve_pack(void* base, const flc_codec_params* prm, int64_t d, size_t* bytes) {
+    Carver c(base);
+    PackWs w;
+    w.dense = c.take<float>((size_t)std::max<int64_t>(d, 1));
+    w.pnorm = c.take<float>(1);
+    w.bc = c.take<uint32_t>((size_t)std::max<int64_t>((d + PK_BLK - 1) / PK_BLK, 1));
+    w.inner_bytes = encode_row_workspace(prm, d);
+    w.inner = c.take<char>(w.inner_bytes);
+    if (bytes) *bytes = c.bytes();
+    return w;
+}
+
+size_t pack_workspace(const flc_codec_params* prm, int64_t d) {
+    size_t b = 0;
+    carve_pack(nullptr, prm, d, &b);
+    return b;
+}
+
+static bool natbug(const flc_codec_params* prm) { return prm->codec == FLC_NAT_DITHERING; }
+
+int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, char* payload, void* ws,
+             size_t ws_bytes, hipStream_t st) {
+    if (ws_bytes < pack_workspace(prm, d)) { set_error("flc_pack: workspace too small"); return FLC_ERR_WORKSPACE; }
+    if ((uintptr_t)payload & 15u) { set_error("flc_pack: payload must be 16-byte aligned"); return FLC_ERR_ARG; }
+    PackWs w = carve_pack(ws, prm, d, nullptr);
+    const int fmt = payload_format(prm);
+    // header zeroed; the body's 16-B padding (and the unused part of a sparse list) zeroed too, so
+    // a payload's bytes are a function of the row alone
+    const int64_t pb = payload_bytes(prm, d);
+    if (fmt == FMT_SPARSE) FLC_CHECK_HIP(hipMemsetAsync(payload, 0, (size_t)pb, st));
+    else {
+        FLC_CHECK_HIP(hipMemsetAsync(payload, 0, 16, st));
+        FLC_CHECK_HIP(hipMemsetAsync(payload + pb - 16, 0, 16, st));
+    }
+    if (d == 0) {
+        PayloadHeader h{(uint32_t)fmt, 0u, 0.f, 0u};
+        FLC_CHECK_HIP(hipMemcpyAsync(payload, &h, sizeof(h), hipMemcpyHostToDevice, st));
+        FLC_CHECK_HIP(hipStreamSynchronize(st));     // h lives on this stack frame
+        return FLC_OK;
+    }
+    const bool dither = fmt == FMT_Q8 || fmt == FMT_Q16;
+    int rc = encode_row(prm, pat, x, d, nullptr, dither ? w.pnorm : nullptr, w.dense, w.inner, w.inner_bytes, st);
+    if (rc) return rc;
+    (void)natbug;
+    if (fmt == FMT_SPARSE) {
+        const int64_t nb = (d + PK_BLK - 1) / PK_BLK, cap = std::max<int64_t>(1, std::min(prm->k, d));
+        hipLaunchKernelGGL(k_pack_count, dim3((unsigned)nb), dim3(256), 0, st, w.dense, d, w.bc);
+        FLC_CHECK_LAUNCH("k_pack_count");
+        hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, st, w.bc, nb, payload, cap);
+        FLC_CHECK_LAUNCH("k_pack_scan");
+        hipLaunchKernelGGL(k_pack_write, dim3((unsigned)nb), dim3(256), 0, st, w.dense, d, w.bc, payload, cap);
+        FLC_CHECK_LAUNCH("k_pack_write");
+        return FLC_OK;
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_pack_dense, dim3(grid), dim3(256), 0, st, w.dense, d, fmt, prm->d_levels, prm->s,
+                       dither ? w.pnorm : nullptr, payload);
+    FLC_CHECK_LAUNCH("k_pack_dense");
+    return FLC_OK;
+}
+
+int unpack_run(const flc_codec_params* prm, const char* payload, int64_t d, float* out, hipStream_t st) {
+    if (d == 0) return FLC_OK;
+    if ((uintptr_t)payload & 15u) { set_error("flc_unpack: payload must be 16-byte aligned"); return FLC_ERR_ARG; }
+    const int fmt = payload_format(prm);
+    if (fmt == FMT_SPARSE) {
+        const int64_t cap = std::max<int64_t>(1, std::min(prm->k, d));
+        FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cap + 255) / 256, 4096));
+        hipLaunchKernelGGL(k_unpack_sparse, dim3(grid), dim3(256), 0, st, payload, cap, out);
+        FLC_CHECK_LAUNCH("k_unpack_sparse");
+        return FLC_OK;
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_unpack_dense, dim3(grid), dim3(256), 0, st, payload, d, prm->d_levels, out);
+    FLC_CHECK_LAUNCH("k_unpack_dense");
+    return FLC_OK;
+}
+
+size_t unpack_reduce_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
+    return payload_format(prm) == FMT_SPARSE ? sel_unpack_workspace(prm, n, d) : 0;
+}
+
+int unpack_reduce_run(const flc_codec_params* prm, const char* base, int64_t ld, const char* const* ptrs, int64_t n,
+                      int64_t d, const float* w, float wt, float* out, void* ws, size_t ws_bytes, hipStream_t st) {
+    if (d == 0) return FLC_OK;
+    if (n == 0) { FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st)); return FLC_OK; }
+    const int fmt = payload_format(prm);
+    if (fmt == FMT_SPARSE) return sel_unpack_reduce(prm, base, ld, (const void* const*)ptrs, n, d, w, wt, out, ws, ws_bytes, st);
+    if (base && ((ld & 15) || ((uintptr_t)base & 15u))) { set_error("flc_unpack_reduce: payload rows must be 16-byte aligned"); return FLC_ERR_ARG; }
+    const int64_t groups = (d + 3) / 4;
+    const int grid = (int)((groups + 255) / 256);
+#define UNPACK_CASE(F)                                                                                      \
+    if (w) hipLaunchKernelGGL((k_unpack_accum<F, true>), dim3(grid), dim3(256), 0, st, base, ld, ptrs, n, d,   \
+                              prm->d_levels, w, wt, out);                                                   \
+    else hipLaunchKernelGGL((k_unpack_accum<F, false>), dim3(grid), dim3(256), 0, st, base, ld, ptrs, n, d,    \
+                            prm->d_levels, w, wt, out);
+    { ProfScope _ps("k_unpack_accum", st);
+    if (fmt == FMT_Q8) { UNPACK_CASE(FMT_Q8) }
+    else if (fmt == FMT_Q16) { UNPACK_CASE(FMT_Q16) }
+    else if (fmt == FMT_NAT16) { UNPACK_CASE(FMT_NAT16) }
+    else { UNPACK_CASE(FMT_F32) } }
+#undef UNPACK_CASE
+    FLC_CHECK_LAUNCH("k_unpack_accum");
+    return FLC_OK;
+}
+
+}  // namespace flc

@@ -160,6 +160,38 @@ int flc_encode_shift(const flc_codec_params* prm, const flc_pattern* pat, const 
                      float* d_pnorm_out, void* d_ws, size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------------------------------------
+ * Wire format: the message a client sends, and the server's decode +
+ * reduce straight from the N messages.  The reference counts these bits
+ * (last_need_to_send_advance, compressors.py:223-224, 367-368) but moves the dense decoded
+ * tensor (comm_socket.py:16-82 pickles it).  One row's payload = 16-B header
+ * {u32 format, u32 count, f32 norm, u32 bad} + body, padded to 16 B:
+ *   1 F32    ident, lazy, natural dithering, rank_k        f32[d]
+ *   2 Q8     std dithering / qsgd / terngrad, s <= 127     u8[d]: bit 7 sign, bits 0-6 level index
+ *   3 Q16    std dithering, s > 127                        u16[d]: bit 15 sign, bits 0-14 level index
+ *   4 NAT16  natural                                       u16[d]: bit 15 sign; 0 zero, 0x7FFE inf,
+ *                                                          0x7FFF NaN, else k + 16384 for 2^k
+ *   5 SPARSE randk, topk                                   u32 idx[K] then f32 val[K] (count used,
+ *                                                          ascending idx, the elements not +0)
+ * Level code 0 is +0; otherwise value = (levels[idx] * sign) * norm (compressors.py:294-296).
+ * flc_unpack(flc_pack(x)) == flc_encode(x) bit for bit; flc_unpack_reduce(payloads) ==
+ * flc_encode_reduce(rows).  flc_pack runs the encode (same patterns and draws as flc_encode)
+ * and derives the codes from its output.  Payloads are 16-byte aligned; strided payload rows
+ * (d_payloads + i * ld_bytes, ld_bytes >= flc_payload_bytes, a multiple of 16) or a device
+ * array of payload pointers.
+ * -------------------------------------------------------------------------------------- */
+int64_t flc_payload_bytes(const flc_codec_params* prm, int64_t d);
+int flc_payload_format(const flc_codec_params* prm);
+size_t flc_pack_workspace_size(const flc_codec_params* prm, int64_t d);
+int flc_pack(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
+             void* d_payload, void* d_ws, size_t ws_bytes, void* stream);
+int flc_unpack(const flc_codec_params* prm, const void* d_payload, int64_t d, float* d_out,
+               void* stream);
+size_t flc_unpack_reduce_workspace_size(const flc_codec_params* prm, int64_t n, int64_t d);
+int flc_unpack_reduce(const flc_codec_params* prm, const void* d_payloads, int64_t ld_bytes,
+                      const void* const* d_payload_ptrs, int64_t n, int64_t d, const float* d_w,
+                      float w_total, float* d_out, void* d_ws, size_t ws_bytes, void* stream);
+
+/* ----------------------------------------------------------------------------------------
  * Host side of compat mode: the numpy legacy MT19937 stream (what the reference's
  * rndgen.choice / rand / random / randint draw, compressors.py:204-212, algorithms.py:2055),
  * advanced in place on a caller-held state (key[624], pos — numpy's get_state() layout).

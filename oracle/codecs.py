@@ -32,12 +32,13 @@ _F32 = np.float32
 
 
 def _levels_std(levels):
-    # torch.arange(0.0, 1.0 + 1.0/levels*0.5, 1.0/levels) (compressors.py:87): fp32 values of
-    # start + i*step computed in double, the length ceil((end-start)/step).
-    step = 1.0 / levels
-    end = 1.0 + step * 0.5
-    n = int(math.ceil((end - 0.0) / step))
-    return np.array([0.0 + i * step for i in range(n)], dtype=np.float64).astype(_F32)
+    # torch.arange(0.0, 1.0 + 1.0/levels*0.5, 1.0/levels) (compressors.py:87).  The reference's
+    # own call, on the CPU: torch's vectorised arange forms start + step * i partly in fp32, so a
+    # float64 restatement differs from it in the last bit for s >= ~300 (s = 300: 259 of 4099
+    # QSGD outputs one ulp apart).  The call is deterministic third-party arithmetic, pinned by the
+    # golden level tables (tests/test_oracle_golden.py::test_codec_constants).
+    import torch
+    return torch.arange(0.0, 1.0 + 1.0 / levels * 0.5, 1.0 / levels, dtype=torch.float32).numpy().copy()
 
 
 def _levels_nat(levels):

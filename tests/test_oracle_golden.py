@@ -194,3 +194,22 @@ def test_shift_step_golden(i):
     if m["alpha"] is not None:
         np.testing.assert_array_equal(h2.view(np.uint32), SH[f"h{i}"].view(np.uint32))
     assert comp.last_need_to_send_advance == m["need"]
+
+
+@pytest.mark.parametrize("i", range(len(CODEC_META)), ids=[f"{m['spec']}-{m['D']}" for m in CODEC_META])
+def test_wire_format_lossless_on_reference_outputs(i):
+    """The wire format (oracle/wire.py == wire.hip's layout) reproduces every reference output of
+    the golden codec cases bit for bit after pack -> unpack (dithering with the reference's norm)."""
+    from oracle import wire
+    m, X, OUT = _case(i)
+    pn = CODEC[f"c{i:02d}_pnorm"]
+    for c in range(m["n_clients"]):
+        comp = oc.OracleCompressor(m["spec"], m["D"])
+        out = OUT[c]
+        p = pn[c] if m["type"] in (5, 6) else None
+        pl = wire.pack(comp, out, p)
+        assert pl.size == wire.payload_bytes(comp, m["D"]) and pl.size % 16 == 0
+        assert pl[12:16].view(np.uint32)[0] == 0                 # no element without a code
+        np.testing.assert_array_equal(wire.unpack(comp, pl, m["D"]).view(np.uint32), out.view(np.uint32))
+        if m["type"] == 5 and comp.s <= 127:
+            assert pl.size <= 16 + m["D"] + 15                   # one byte per element
