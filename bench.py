@@ -170,6 +170,58 @@ def e2e(args):
                       "note": "rows start in pinned host memory; 2-stream H2D/encode overlap, blocks of 8 clients"}))
 
 
+def wire(args):
+    """Server side from the wire format: N client payloads already in HBM
+    (qsgd:127 -> 1 byte per element + 16-B header, C4's shard shape by default) decoded and folded
+    into the [D] mean (flc_unpack_reduce).  Reported on its own line, never as `value`."""
+    from flpytorch_amd import _lib
+    from flpytorch_amd import aggregation as ag
+    wl = dict(WORKLOADS[args.workload])
+    n, d = args.n or wl["n"], args.d or wl["d"]
+    spec = wl["spec"] if wl["spec"] != "mixed" else "qsgd:127"
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    pool = min(n, 16)
+    gen = torch.Generator(device=dev).manual_seed(77)
+    comps = []
+    c0 = ag.initCompressor(spec, d)
+    ld = c0.payloadBytes()
+    pay = torch.empty((n, ld), dtype=torch.uint8, device=dev)
+    x = torch.empty(d, dtype=torch.float32, device=dev)
+    rs = np.random.RandomState(5)
+    for i in range(pool):
+        x.normal_(generator=gen)
+        c = ag.initCompressor(spec, d)
+        c.device_rng = (20241015, i)
+        c.compressPayload(x, out=pay[i])
+        comps.append(c)
+    for i in range(pool, n):
+        pay[i].copy_(pay[i % pool])
+    red = ag.PayloadReducer(c0, device=dev)
+    out = torch.empty(d, dtype=torch.float32, device=dev)
+    for _ in range(args.warmup):
+        red(pay, d=d, out=out)
+    torch.cuda.synchronize()
+    _lib.profile_enable(True)
+    _lib.profile_collect("k_unpack_accum")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        red(pay, d=d, out=out)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    _lib.profile_enable(False)
+    kms, kn = _lib.profile_collect("k_unpack_accum")
+    moved = n * ld + 4 * d
+    kern = moved / (kms / max(kn, 1) * 1e-3) / 1e9 if kn else None
+    print(json.dumps({"mode": "server decode+reduce from wire payloads (flc_unpack_reduce)", "codec": spec,
+                      "clients": n, "D": d, "payload_bytes_per_client": ld,
+                      "dense_bytes_per_client": 4 * d, "ms_per_step": round(dt * 1e3, 3),
+                      "payload_GBps": round(moved / dt / 1e9, 1),
+                      "dense_equivalent_GBps": round((4 * n * d + 4 * d) / dt / 1e9, 1),
+                      "kernel": "k_unpack_accum", "kernel_GBps": round(kern, 1) if kern else None,
+                      "note": f"{pool} distinct payloads replicated to {n} rows; device-RNG draws"}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,12 +231,16 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--wire", action="store_true",
+                    help="server side from the wire format: decode+reduce of N resident payloads (own line, not value)")
     ap.add_argument("--e2e", action="store_true",
                     help="end-to-end: client rows start in pinned host memory, the [D] result lands in host memory "
                          "(H2D + encode+reduce + D2H per step; PCIe-bound; reported in DESIGN.md, never as value)")
     args = ap.parse_args()
     if args.e2e:
         return e2e(args)
+    if args.wire:
+        return wire(args)
 
     wl = dict(WORKLOADS[args.workload])
     if args.n:

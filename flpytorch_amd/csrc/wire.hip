@@ -217,59 +217,110 @@ __global__ __launch_bounds__(256) void k_unpack_sparse(const char* __restrict__ 
 }
 
 // ---- decode + reduce over n payloads (dense formats) --------------------------------------------
-// Tile owner: each thread owns 4 consecutive columns for the whole fold, rows in order, so the fp32
-// sum is the sequential one: acc = t_0; acc = acc + t_i; out = acc / wt  (t_i = w_i * dec_i).
-template <int FMT, bool W>
+// Tile owner: each thread owns the E elements of one 16-B body slice (E = 16 Q8 codes, 8 Q16 /
+// NAT16 codes, 4 floats) for the whole fold, rows in order, PF rows' slices in flight (a register
+// ring), so the fp32 sum is the sequential one: acc = t_0; acc = acc + t_i; out = acc / wt with
+// t_i = w_i * dec_i.  Q8 level tables (<= 128 levels) sit in LDS.
+template <int FMT>
+struct WireFmt {
+    static constexpr int E = FMT == FMT_Q8 ? 16 : (FMT == FMT_F32 ? 4 : 8);
+    static constexpr int BYTES = 16 / E;
+};
+
+template <int FMT>
+__device__ inline float dec1(uint32_t c, const float* lv, float norm) {
+    if (FMT == FMT_Q8) return lev_decode(c, lv, norm, 0x80u);
+    if (FMT == FMT_Q16) return lev_decode(c, lv, norm, 0x8000u);
+    if (FMT == FMT_NAT16) return nat_decode(c);
+    return __uint_as_float(c);
+}
+
+template <int FMT>
+__device__ inline void dec16(uint4 v, const float* lv, float norm, float* e) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    constexpr int E = WireFmt<FMT>::E;
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+        uint32_t c;
+        if (FMT == FMT_Q8) c = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+        else if (FMT == FMT_F32) c = w[q];
+        else c = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        e[q] = dec1<FMT>(c, lv, norm);
+    }
+}
+
+template <int FMT, bool W, int PF>
 __global__ __launch_bounds__(256) void k_unpack_accum(const char* __restrict__ base, int64_t ld,
                                                       const char* const* __restrict__ ptrs, int64_t n, int64_t d,
-                                                      const float* __restrict__ levels, const float* __restrict__ w,
-                                                      float wt, float* __restrict__ out) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t j0 = g * 4;
-    if (j0 >= d) return;
-    const int m = (int)min<int64_t>(4, d - j0);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t i = 0; i < n; ++i) {
-        const char* p = base ? base + i * ld : sload(ptrs + i);
-        const float norm = (FMT == FMT_Q8 || FMT == FMT_Q16) ? sload(reinterpret_cast<const float*>(p + 8)) : 0.f;
-        const float wi = W ? w[i] : 1.f;
-        float e[4];
-        const char* body = p + 16;
-        if (FMT == FMT_Q8) {
-            uint32_t c4;
-            if (m == 4) c4 = *reinterpret_cast<const uint32_t*>(body + j0);
-            else { c4 = 0; for (int q = 0; q < m; ++q) c4 |= (uint32_t)reinterpret_cast<const uint8_t*>(body)[j0 + q] << (8 * q); }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) e[q] = lev_decode((c4 >> (8 * q)) & 0xFFu, levels, norm, 0x80u);
-        } else if (FMT == FMT_Q16 || FMT == FMT_NAT16) {
-            uint2 c2;
-            if (m == 4) c2 = *reinterpret_cast<const uint2*>(body + 2 * j0);
-            else {
-                uint32_t c[4] = {0, 0, 0, 0};
-                for (int q = 0; q < m; ++q) c[q] = reinterpret_cast<const uint16_t*>(body)[j0 + q];
-                c2 = make_uint2(c[0] | (c[1] << 16), c[2] | (c[3] << 16));
-            }
-            const uint32_t cc[4] = {c2.x & 0xFFFFu, c2.x >> 16, c2.y & 0xFFFFu, c2.y >> 16};
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                e[q] = FMT == FMT_NAT16 ? nat_decode(cc[q]) : lev_decode(cc[q], levels, norm, 0x8000u);
-        } else {
-            float4 v;
-            if (m == 4) v = *reinterpret_cast<const float4*>(body + 4 * j0);
-            else {
-                float t[4] = {0.f, 0.f, 0.f, 0.f};
-                for (int q = 0; q < m; ++q) t[q] = reinterpret_cast<const float*>(body)[j0 + q];
-                v = make_float4(t[0], t[1], t[2], t[3]);
-            }
-            e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float t = W ? wi * e[q] : e[q];
-            acc[q] = (i == 0) ? t : acc[q] + t;
-        }
+                                                      const float* __restrict__ levels, int s,
+                                                      const float* __restrict__ w, float wt, float* __restrict__ out) {
+    constexpr int E = WireFmt<FMT>::E;
+    __shared__ float lvs[128];
+    const float* lv = levels;
+    if (FMT == FMT_Q8) {
+        for (int i = threadIdx.x; i <= s && i < 128; i += 256) lvs[i] = levels[i];
+        __syncthreads();
+        lv = lvs;
     }
-    for (int q = 0; q < m; ++q) out[j0 + q] = acc[q] / wt;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t j0 = g * E;
+    const int64_t full = d / E;                       // complete 16-B slices
+    auto row = [&](int64_t i) -> const char* { return base ? base + i * ld : sload(ptrs + i); };
+    if (g < full) {
+        uint4 ring[PF];
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+            if (p < n) ring[p] = *reinterpret_cast<const uint4*>(row(p) + 16 + g * 16);
+        float acc[E];
+        for (int64_t i0 = 0; i0 < n; i0 += PF) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) {
+                const int64_t i = i0 + p;
+                if (i < n) {
+                    const char* r = row(i);
+                    const float norm = (FMT == FMT_Q8 || FMT == FMT_Q16) ? sload(reinterpret_cast<const float*>(r + 8)) : 0.f;
+                    const float wi = W ? w[i] : 1.f;
+                    float e[E];
+                    dec16<FMT>(ring[p], lv, norm, e);
+                    if (i + PF < n) ring[p] = *reinterpret_cast<const uint4*>(row(i + PF) + 16 + g * 16);
+#pragma unroll
+                    for (int q = 0; q < E; ++q) {
+                        const float t = W ? wi * e[q] : e[q];
+                        acc[q] = (i == 0) ? t : acc[q] + t;
+                    }
+                }
+            }
+        }
+        float4* o4 = reinterpret_cast<float4*>(out + j0);
+        if (((uintptr_t)(out + j0) & 15u) == 0) {
+#pragma unroll
+            for (int q = 0; q < E; q += 4) o4[q / 4] = make_float4(acc[q] / wt, acc[q + 1] / wt, acc[q + 2] / wt, acc[q + 3] / wt);
+        } else {
+#pragma unroll
+            for (int q = 0; q < E; ++q) out[j0 + q] = acc[q] / wt;
+        }
+        return;
+    }
+    if (g == full && full * E < d) {                   // the tail: fewer than E elements, element loads
+        const int m = (int)(d - full * E);
+        float acc[E];
+        for (int64_t i = 0; i < n; ++i) {
+            const char* r = row(i);
+            const float norm = (FMT == FMT_Q8 || FMT == FMT_Q16) ? reinterpret_cast<const float*>(r + 8)[0] : 0.f;
+            const float wi = W ? w[i] : 1.f;
+            for (int q = 0; q < m; ++q) {
+                const int64_t j = full * E + q;
+                uint32_t c;
+                if (FMT == FMT_Q8) c = reinterpret_cast<const uint8_t*>(r + 16)[j];
+                else if (FMT == FMT_F32) c = reinterpret_cast<const uint32_t*>(r + 16)[j];
+                else c = reinterpret_cast<const uint16_t*>(r + 16)[j];
+                const float e = dec1<FMT>(c, lv, norm);
+                const float t = W ? wi * e : e;
+                acc[q] = (i == 0) ? t : acc[q] + t;
+            }
+        }
+        for (int q = 0; q < m; ++q) out[full * E + q] = acc[q] / wt;
+    }
 }
 
 // ---- host ----------------------------------------------------------------------------------------
@@ -370,13 +421,15 @@ int unpack_reduce_run(const flc_codec_params* prm, const char* base, int64_t ld,
     const int fmt = payload_format(prm);
     if (fmt == FMT_SPARSE) return sel_unpack_reduce(prm, base, ld, (const void* const*)ptrs, n, d, w, wt, out, ws, ws_bytes, st);
     if (base && ((ld & 15) || ((uintptr_t)base & 15u))) { set_error("flc_unpack_reduce: payload rows must be 16-byte aligned"); return FLC_ERR_ARG; }
-    const int64_t groups = (d + 3) / 4;
+    const int E = fmt == FMT_Q8 ? 16 : (fmt == FMT_F32 ? 4 : 8);
+    const int64_t groups = d / E + 1;
     const int grid = (int)((groups + 255) / 256);
-#define UNPACK_CASE(F)                                                                                      \
-    if (w) hipLaunchKernelGGL((k_unpack_accum<F, true>), dim3(grid), dim3(256), 0, st, base, ld, ptrs, n, d,   \
-                              prm->d_levels, w, wt, out);                                                   \
-    else hipLaunchKernelGGL((k_unpack_accum<F, false>), dim3(grid), dim3(256), 0, st, base, ld, ptrs, n, d,    \
-                            prm->d_levels, w, wt, out);
+    if (fmt == FMT_Q8 && prm->s > 127) { set_error("flc_unpack_reduce: Q8 with s > 127"); return FLC_ERR_ARG; }
+#define UNPACK_CASE(F)                                                                                       \
+    if (w) hipLaunchKernelGGL((k_unpack_accum<F, true, 4>), dim3(grid), dim3(256), 0, st, base, ld, ptrs, n, d,  \
+                              prm->d_levels, prm->s, w, wt, out);                                            \
+    else hipLaunchKernelGGL((k_unpack_accum<F, false, 4>), dim3(grid), dim3(256), 0, st, base, ld, ptrs, n, d,   \
+                            prm->d_levels, prm->s, w, wt, out);
     { ProfScope _ps("k_unpack_accum", st);
     if (fmt == FMT_Q8) { UNPACK_CASE(FMT_Q8) }
     else if (fmt == FMT_Q16) { UNPACK_CASE(FMT_Q16) }
