@@ -432,6 +432,9 @@ def main():
                        "clients_per_gpu": n, "clients_total": n * world, "D": d, "K": k,
                        "parallelism": f"client-shard dp{world}" + (" + RCCL all-reduce" if world > 1 else "")},
             "pct_hbm_peak": round(100.0 * value / world / PEAK_GBS, 2),
+            # RandK also reports the dense-equivalent rate 4 N D / t (never the roofline)
+            "dense_equivalent_GBps": round((4 * n * d + 4 * d) * world / (elapsed / args.steps) / 1e9, 1)
+            if (spec.startswith("randk") or mixed) else None,
             "roofline": {"bound": "hbm", "kernel": wl["kernel"],
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBS, 4) if achieved else None, "traffic": traffic,

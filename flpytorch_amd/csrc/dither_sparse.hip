@@ -148,9 +148,8 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // 3 loads only (a running xor keeps them alive); 4 full but no copy-out of the staged entries;
 // 5 copy-out into one fixed per-wave scratch region (L2-resident: stores without HBM traffic);
 // 6 full with non-temporal copy-out stores
-template <int RING, int GCAP, int PROBE = 0>
+template <int RING, int GCAP, int PROBE = 0, int FGS = DS_FGS>
 __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, DsWs ws) {
-    constexpr int FGS = DS_FGS;
     constexpr int NH = 2 * FGS;                               // half chunks per item
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     static_assert(GCAP % 128 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
@@ -561,23 +560,24 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
 // ------------------------------------------------------------------------------------------
 // Filter variant (tuning runs: FLC_DS_GCAP=1024 doubles the per-item staging and list regions,
 // FLC_DS_GRID=res launches a resident-only grid instead of the oversubscribed one).
-struct DsVariant { int gcap; bool resident; int ap; };
+struct DsVariant { int gcap; bool resident; int ap; int fgs; };
 static DsVariant ds_variant() {
-    DsVariant v{DS_GCAP, false, DS_AP};
+    DsVariant v{DS_GCAP, false, DS_AP, DS_FGS};
+    if (const char* e = getenv("FLC_DS_FGS")) v.fgs = atoi(e) == 4 ? 4 : DS_FGS;
     if (const char* e = getenv("FLC_DS_AP")) v.ap = atoi(e);
     if (const char* e = getenv("FLC_DS_GCAP")) v.gcap = atoi(e) == 1024 ? 1024 : DS_GCAP;
     if (const char* e = getenv("FLC_DS_GRID")) v.resident = !strcmp(e, "res");
     return v;
 }
 
-static DsWs carve_ds(void* base, int64_t n, int64_t d, int gcap, size_t* bytes) {
+static DsWs carve_ds(void* base, int64_t n, int64_t d, int gcap, int fgs, size_t* bytes) {
     Carver cv(base);
     const int64_t C = std::max<int64_t>(nchunks(d), 1), H = std::max<int64_t>(nhalves(d), 1);
     const int64_t nn = std::max<int64_t>(n, 1);
     DsWs w;
-    w.G = (C + DS_FGS - 1) / DS_FGS;
+    w.G = (C + fgs - 1) / fgs;
     w.cap = w.G * gcap;
-    w.tab = cv.take<uint2>((size_t)std::max<int64_t>(H, w.G * 2 * DS_FGS) * nn);   // + padding halves
+    w.tab = cv.take<uint2>((size_t)std::max<int64_t>(H, w.G * 2 * fgs) * nn);   // + padding halves
     w.ent = cv.take<uint2>((size_t)nn * w.cap);
     w.ovfi = cv.take<uint32_t>((size_t)nn * w.G);
     w.flags = cv.take<uint32_t>(nn);
@@ -617,7 +617,7 @@ bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n,
 size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     (void)prm;
     size_t b = 0;
-    carve_ds(nullptr, n, d, ds_variant().gcap, &b);
+    carve_ds(nullptr, n, d, ds_variant().gcap, ds_variant().fgs, &b);
     return b;
 }
 
@@ -641,9 +641,9 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
            float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
     const DsVariant v = ds_variant();
     size_t need = 0;
-    carve_ds(nullptr, n, d, v.gcap, &need);
+    carve_ds(nullptr, n, d, v.gcap, v.fgs, &need);
     if (ws_bytes < need) { set_error("dithering (sparse): workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
-    DsWs ws = carve_ds(wsp, n, d, v.gcap, nullptr);
+    DsWs ws = carve_ds(wsp, n, d, v.gcap, v.fgs, nullptr);
     const int64_t client0 = pat ? pat->client0 : 0;
     const int64_t H = nhalves(d);
     const char* pe = getenv("FLC_DS_PROBE");
@@ -668,6 +668,8 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         if (probe == 2) launch(k_ds_filter<16, DS_GCAP, 2>);
         else if (probe == 3) launch(k_ds_filter<16, DS_GCAP, 3>);
         else if (probe == 4) launch(k_ds_filter<16, DS_GCAP, 4>);
+        else if (v.fgs == 4 && v.gcap == 1024) launch(k_ds_filter<16, 1024, 0, 4>);
+        else if (v.fgs == 4) launch(k_ds_filter<16, DS_GCAP, 0, 4>);
         else if (v.gcap == 1024) launch(k_ds_filter<16, 1024>);
         else launch(k_ds_filter<16, DS_GCAP>);
         FLC_CHECK_LAUNCH("k_ds_filter");
