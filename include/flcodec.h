@@ -35,7 +35,7 @@ typedef enum {
     FLC_ERR_DTYPE = 2,      /* not fp32 */
     FLC_ERR_HIP = 3,        /* a HIP runtime call failed (launch, memset) */
     FLC_ERR_WORKSPACE = 4,  /* workspace smaller than *_workspace_size() */
-    FLC_ERR_UNSUPPORTED = 5 /* codec / mode not built (e.g. rank_k) */
+    FLC_ERR_UNSUPPORTED = 5 /* codec / mode not supported (e.g. a p-norm other than 1, 2, inf) */
 } flc_status;
 
 /* Codec ids = the reference's CompressorType values (compressors.py:11-19). */

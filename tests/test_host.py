@@ -133,3 +133,24 @@ def test_device_rng_oracle_restatement():
     u = devrng.dev_u32(7, 1, np.arange(1 << 16, dtype=np.uint32))
     top = (u >> np.uint32(24)).astype(np.int64)
     assert abs(top.mean() - 127.5) < 2.0 and np.unique(top).size == 256
+
+
+def test_c_client_of_the_abi(tmp_path):
+    """include/flcodec.h compiles as C99 (-pedantic, no warnings) and a C program linked against
+    libflcodec.so gets the same host-side answers as the Python binding (tests/c/abi_host.c)."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    root = os.path.join(os.path.dirname(__file__), "..")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    exe = str(tmp_path / "abi_host")
+    cc = subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                         "-I" + os.path.join(root, "include"), os.path.join(root, "tests", "c", "abi_host.c"),
+                         "-L" + libdir, "-lflcodec", "-Wl,-rpath," + libdir, "-o", exe],
+                        capture_output=True, text=True)
+    assert cc.returncode == 0, cc.stderr
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert "OK" in run.stdout
