@@ -10,12 +10,16 @@ from .compressors import (Compressor, CompressorType, initCompressor, stream_cho
 from .fused import PayloadReducer, UplinkReducer  # noqa: F401
 from .mixed import MixedUplink  # noqa: F401
 from .shift import dianaStep, ef21Step, marinaStep  # noqa: F401
-from .reduce import (reduce_client_models, reduce_rows, serverGradientMaster,  # noqa: F401
-                     serverGradientPlain)
+from .reduce import (reduce_client_models, reduce_rows, serverGradientCOFIG,  # noqa: F401
+                     serverGradientDIANA, serverGradientMaster, serverGradientPlain)
 
 # Algorithm classes whose serverGradient is exactly the shared fold, and what follows it.
-PLAIN_FOLD = ("FedAvg", "FedProx")                  # return gs            (1810-1832, 1886-1908)
-MASTER_FOLD = ("DCGD", "EF21")                      # master compressor    (1748-1770, 1521-1546)
+PLAIN_FOLD = ("FedAvg", "FedProx",                  # return gs            (1810-1832, 1886-1908,
+              "MarinaAlgorithm", "MarinaAlgorithmPP", "SCAFFOLD")  #        545-563, 699-717, 792-814)
+MASTER_FOLD = ("DCGD", "EF21", "EF21PP")            # master compressor    (1748-1770, 1521-1546, 1654-1679)
+SHIFTED_FOLD = {"DIANA": serverGradientDIANA,       # H['m'] = gs; h + gs  (1395-1421)
+                "COFIG": serverGradientCOFIG}       # u + h_prev, updates  (1273-1307)
+# Not rebound: GradSkip (951-998) and FRECON (1124-1176) fold other per-client vectors as well.
 
 
 def install(compressors_module, algorithms_module=None):
@@ -27,7 +31,8 @@ def install(compressors_module, algorithms_module=None):
     compressors_module.initCompressor = initCompressor
     compressors_module.Compressor = Compressor
     if algorithms_module is not None:
-        for name, fn in [(n, serverGradientPlain) for n in PLAIN_FOLD] + [(n, serverGradientMaster) for n in MASTER_FOLD]:
+        for name, fn in ([(n, serverGradientPlain) for n in PLAIN_FOLD] + [(n, serverGradientMaster) for n in MASTER_FOLD]
+                         + list(SHIFTED_FOLD.items())):
             cls = getattr(algorithms_module, name, None)
             if cls is None:
                 continue

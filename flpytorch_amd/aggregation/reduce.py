@@ -111,3 +111,25 @@ def make_server_gradient(master_compress):
 
 serverGradientPlain = make_server_gradient(False)
 serverGradientMaster = make_server_gradient(True)
+
+
+def serverGradientDIANA(clients_responses, clients, model, params_current, H):
+    """DIANA.serverGradient (algorithms.py:1395-1421): the fold gs, recorded as H['m'] (the
+    estimator without shift), returned shifted: H['h'] + gs."""
+    gs = reduce_client_models(clients_responses, clients, params_current, H)
+    H['m'] = gs
+    return H['h'] + gs
+
+
+def serverGradientCOFIG(clients_responses, clients, model, params_current, H):
+    """COFIG.serverGradient (algorithms.py:1273-1307): the fold u = gs, returned as u + H['h_prev'];
+    H['u_avg_update'] = u and H['alpha_update'] = alpha * (clients / H['total_clients']) with alpha
+    the first response's client_state['alpha'] (for serverGlobalStateUpdate)."""
+    if clients == 0:
+        return torch.zeros_like(params_current)
+    gs = reduce_client_models(clients_responses, clients, params_current, H)
+    alpha = clients_responses.get(0)["client_state"]['alpha']
+    result = gs + H['h_prev']
+    H['u_avg_update'] = gs
+    H['alpha_update'] = alpha * (clients / H['total_clients'])
+    return result

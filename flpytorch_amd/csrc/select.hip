@@ -1045,18 +1045,22 @@ __device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64
 }
 
 
-template <bool ASSIGN>
+// TS < CHUNK: a wave owns TS columns of a chunk (CHUNK / TS waves read the same lists and each
+// folds its part): a smaller LDS tile per wave, so more waves per CU hide the list latency.
+template <bool ASSIGN, int TS = CHUNK>
 __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
                                                      float wt, float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float tile[4][CHUNK];
+    constexpr int PARTS = CHUNK / TS;
+    __shared__ __attribute__((aligned(16))) float tile[4][TS];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t C = nchunks(d);
     float* tl = tile[wv];
     const int64_t nb = (n + 63) / 64;                  // row batches
-    for (int64_t c = (int64_t)blockIdx.x * 4 + wv; c < C; c += (int64_t)gridDim.x * 4) {
-        for (int i = lane; i < CHUNK; i += 64) tl[i] = 0.f;
-        const uint32_t cbase = (uint32_t)(c * CHUNK);
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < C * PARTS; t += (int64_t)gridDim.x * 4) {
+        const int64_t c = t / PARTS;
+        for (int i = lane; i < TS; i += 64) tl[i] = 0.f;
+        const uint32_t cbase = (uint32_t)(c * CHUNK + (t % PARTS) * TS);
         RowMeta cur = load_meta(ws, c, n, lane, w), nxt;
         // ring of AP rows' entries (the first 128 of each list; range-checked buffer loads, lanes
         // past the list end get index ~0 = no column)
@@ -1075,9 +1079,9 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
             }
         };
         auto fold = [&](uint32_t ix, float vv, uint32_t T, uint32_t cut, uint32_t mode, float wi) {
-            const uint32_t loc = ix - cbase;                   // ~0 index: loc >= CHUNK
+            const uint32_t loc = ix - cbase;                   // ~0 index / other part: loc >= TS
             const uint32_t key = mag_key(vv);
-            if (loc < (uint32_t)CHUNK && (mode == 2u || key > T || (key == T && ix <= cut))) {
+            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut))) {
                 if (ASSIGN) tl[loc] = vv;
                 else tl[loc] = tl[loc] + wi * vv;
             }
@@ -1139,7 +1143,7 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
             }
             cur = nxt;
         }
-        const int64_t len = min((int64_t)CHUNK, d - (int64_t)cbase);
+        const int64_t len = min((int64_t)TS, d - (int64_t)cbase);
         for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
     }
 }
@@ -1198,6 +1202,14 @@ static int grid_stride_blocks(int64_t items, int64_t cap = 4096) {
 }
 
 // Runs the TopK / RandK pipeline for n rows and writes out (ASSIGN: n == 1 dense encode).
+static int accum_parts() {
+    static const int p = [] {
+        const char* e = getenv("FLC_ACCUM_PARTS");   // tuning runs only
+        return (e && atoi(e) == 1) ? 1 : (e && atoi(e) == 2) ? 2 : 1;
+    }();
+    return p;
+}
+
 static int filter_group() {
     static const int g = [] {
         const char* e = getenv("FLC_FILTER_GS");     // tuning runs only
@@ -1304,10 +1316,16 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
-    const int ab = grid_stride_blocks((C + 3) / 4, 4096);
     { ProfScope _ps("k_chunk_accum", st);
-if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out); }
+    if (accum_parts() == 2) {
+        const int ab = grid_stride_blocks((2 * C + 3) / 4, 8192);
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    } else {
+        const int ab = grid_stride_blocks((C + 3) / 4, 4096);
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    } }
     FLC_CHECK_LAUNCH("k_chunk_accum");
     return FLC_OK;
 }

@@ -351,3 +351,35 @@ def test_randk_large_rows(ag, mode, d, k):
     kw = {} if mode == "device" else {"randk_idx": torch.from_numpy(np.stack(idx)).cuda()}
     got = red(torch.from_numpy(rows).cuda(), client0=client0, **kw)
     assert_bitexact(got, want)
+
+
+@pytest.mark.parametrize("name", sorted(RUN_META))
+def test_shifted_server_gradients(ag, name):
+    """DIANA (algorithms.py:1395-1421) and COFIG (1273-1307) on the run captures: the fold is the
+    reference's gs bit for bit, then the same torch tail."""
+
+    class Buf:
+        def __init__(self, items):
+            self.items = items
+
+        def waitForItem(self):
+            pass
+
+        def get(self, i):
+            return self.items[i]
+    x = RUNS[f"{name}_r0_x"]
+    models = RUNS[f"{name}_r0_models"]
+    gs_ref = torch.from_numpy(RUNS[f"{name}_r0_gs"].copy()).cuda()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    h = torch.randn(x.size, generator=g, device="cuda")
+    items = [{"model": torch.from_numpy(m.copy()).cuda(), "client_state": {"weight": 1.0, "alpha": 0.37}} for m in models]
+    xt = torch.from_numpy(x.copy()).cuda()
+    H = {"fl_dtype": torch.float32, "h": h}
+    out = ag.serverGradientDIANA(Buf(items), len(items), None, xt, H)
+    assert_bitexact(H["m"], gs_ref.cpu().numpy())
+    assert_bitexact(out, (h + gs_ref).cpu().numpy())
+    H = {"fl_dtype": torch.float32, "h_prev": h, "total_clients": 10}
+    out = ag.serverGradientCOFIG(Buf(items), len(items), None, xt, H)
+    assert_bitexact(out, (gs_ref + h).cpu().numpy())
+    assert_bitexact(H["u_avg_update"], gs_ref.cpu().numpy())
+    assert H["alpha_update"] == 0.37 * (len(items) / 10)

@@ -154,3 +154,34 @@ def test_c_client_of_the_abi(tmp_path):
     run = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert run.returncode == 0, run.stdout + run.stderr
     assert "OK" in run.stdout
+
+
+def test_install_rebinds_every_shared_fold():
+    """install() rebinds the reference classes whose serverGradient is the shared fold
+    (algorithms.py: FedAvg, FedProx, MARINA, PP-MARINA, SCAFFOLD plain; DCGD, EF21, EF21PP with the
+    master compressor; DIANA, COFIG shifted) and restores them."""
+    import types
+    names = ["FedAvg", "FedProx", "MarinaAlgorithm", "MarinaAlgorithmPP", "SCAFFOLD", "DCGD", "EF21", "EF21PP",
+             "DIANA", "COFIG", "GradSkip", "FRECON"]
+    orig = {}
+    algos = types.SimpleNamespace()
+    for n in names:
+        def sg(*a, _n=n):
+            return _n
+        orig[n] = sg
+        setattr(algos, n, type(n, (), {"serverGradient": staticmethod(sg)}))
+    comps = types.SimpleNamespace(initCompressor=lambda *a: "ref", Compressor=object)
+    restore = ag.install(comps, algos)
+    assert comps.initCompressor is ag.initCompressor
+    want = {**{n: ag.serverGradientPlain for n in ag.PLAIN_FOLD}, **{n: ag.serverGradientMaster for n in ag.MASTER_FOLD},
+            **ag.SHIFTED_FOLD}
+    for n in names:
+        fn = getattr(algos, n).serverGradient
+        if n in want:
+            assert fn is want[n], n
+        else:
+            assert fn is orig[n], n                     # GradSkip / FRECON keep the reference's
+    restore()
+    for n in names:
+        assert getattr(algos, n).serverGradient is orig[n]
+    assert comps.initCompressor() == "ref"
