@@ -10,16 +10,19 @@ from .compressors import (Compressor, CompressorType, initCompressor, stream_cho
 from .fused import PayloadReducer, UplinkReducer  # noqa: F401
 from .mixed import MixedUplink  # noqa: F401
 from .shift import dianaStep, ef21Step, marinaStep  # noqa: F401
-from .reduce import (reduce_client_models, reduce_rows, serverGradientCOFIG,  # noqa: F401
-                     serverGradientDIANA, serverGradientMaster, serverGradientPlain)
+from .reduce import (make_server_gradient_frecon, reduce_client_models, reduce_rows,  # noqa: F401
+                     serverGradientCOFIG, serverGradientDIANA, serverGradientGradSkip, serverGradientMaster,
+                     serverGradientPlain)
 
 # Algorithm classes whose serverGradient is exactly the shared fold, and what follows it.
 PLAIN_FOLD = ("FedAvg", "FedProx",                  # return gs            (1810-1832, 1886-1908,
               "MarinaAlgorithm", "MarinaAlgorithmPP", "SCAFFOLD")  #        545-563, 699-717, 792-814)
 MASTER_FOLD = ("DCGD", "EF21", "EF21PP")            # master compressor    (1748-1770, 1521-1546, 1654-1679)
 SHIFTED_FOLD = {"DIANA": serverGradientDIANA,       # H['m'] = gs; h + gs  (1395-1421)
-                "COFIG": serverGradientCOFIG}       # u + h_prev, updates  (1273-1307)
-# Not rebound: GradSkip (951-998) and FRECON (1124-1176) fold other per-client vectors as well.
+                "COFIG": serverGradientCOFIG,       # u + h_prev, updates  (1273-1307)
+                "GradSkip": serverGradientGradSkip}  # fold of x_i - h_i gamma / p, delta_x   (951-998)
+# FRECON (1124-1176) folds the clients' q_i as well and takes lambda from the reference module's
+# experiment-option helpers: its serverGradient is built per installed module.
 
 
 def install(compressors_module, algorithms_module=None):
@@ -38,6 +41,10 @@ def install(compressors_module, algorithms_module=None):
                 continue
             saved.append((cls, "serverGradient", cls.__dict__["serverGradient"]))
             cls.serverGradient = staticmethod(fn)
+        frecon = getattr(algorithms_module, "FRECON", None)
+        if frecon is not None:
+            saved.append((frecon, "serverGradient", frecon.__dict__["serverGradient"]))
+            frecon.serverGradient = staticmethod(make_server_gradient_frecon(algorithms_module))
 
     def restore():
         for obj, attr, val in reversed(saved):

@@ -121,6 +121,93 @@ def serverGradientDIANA(clients_responses, clients, model, params_current, H):
     return H['h'] + gs
 
 
+def serverGradientGradSkip(clients_responses, clients, model, params_current, H):
+    """GradSkip.serverGradient (algorithms.py:951-998): per client the bookkeeping of the
+    reference (local_steps, shift refresh), the fold of x - (x_i - h_i * gamma / p) on MI355X,
+    then delta_x = (x - gs) - x_i per client."""
+    if clients == 0:
+        return torch.zeros_like(params_current)
+    for i in range(clients):
+        clients_responses.waitForItem()
+        cs = clients_responses.get(i)['client_state']
+        cs['local_steps'].append(cs['Ki'])
+        if cs['change_shift']:
+            cs['hi'] = cs['grad']
+            cs['stats']['send_scalars_to_master'] += 1
+            cs['local_steps'][-1] += 1
+    gamma = H['args'].local_lr
+    fl_dtype = H["fl_dtype"]
+    dev = params_current.device
+    rows, weights = [], []
+    for i in range(clients):
+        cm = clients_responses.get(i)
+        m = cm["model"].to(device=dev, dtype=fl_dtype) - cm['client_state']['hi'] * gamma / H['p']
+        rows.append(m)
+        weights.append(cm['client_state']['weight'])
+    view = _ResponseView(rows, weights)
+    gs = reduce_client_models(view, clients, params_current, H)
+    x_mean = params_current - gs
+    for i in range(clients):
+        cm = clients_responses.get(i)
+        cm['client_state']['delta_x'] = x_mean - cm["model"].to(device=dev, dtype=fl_dtype)
+    return gs
+
+
+def make_server_gradient_frecon(algorithms_module):
+    """FRECON.serverGradient (algorithms.py:1124-1176): the model fold u and the fold of the
+    clients' q_i (both on MI355X, client order), then
+    q_avg + (1 - lambda) g_server_prev + lambda (u + h_prev) with lambda from the experiment options
+    through the reference module's own helpers."""
+    am = algorithms_module
+
+    def serverGradient(clients_responses, clients, model, params_current, H):
+        if clients == 0:
+            return torch.zeros_like(params_current)
+        u = reduce_client_models(clients_responses, clients, params_current, H)
+        first = clients_responses.get(0)
+        alpha = first["client_state"]['alpha']
+        qs, weights = [], []
+        for i in range(clients):
+            cs = clients_responses.get(i)['client_state']
+            qs.append(cs['qi'].to(device=u.device, dtype=H["fl_dtype"]).reshape(-1))
+            weights.append(cs['weight'])
+        q_avg = reduce_rows(u.reshape(-1), qs, weights, relative=False).reshape(u.shape)   # x: shape only
+        for i in range(clients):
+            del clients_responses.get(i)['client_state']['qi']
+        h_prev = H['h_prev']
+        if am.has_experiment_option(H, "lambda_"):
+            lambda_ = am.get_experiment_option_f(H, "lambda_")
+        elif am.has_experiment_option(H, "th_stepsize_noncvx") or am.has_experiment_option(H, "th_stepsize_cvx"):
+            S = clients
+            w = am.compressors.initCompressor(H["client_compressor"], H["D"]).getW()
+            n = H['total_clients']
+            H["lambda_th"] = S / (2 * (1 + w) * n)
+            lambda_ = S / (2 * (1 + w) * n)
+            am.get_logger(H).info(f"Used lambda is {lambda_}")
+        else:
+            raise UnboundLocalError("local variable 'lambda_' referenced before assignment")   # as the reference
+        result = q_avg + (1.0 - lambda_) * H["g_server_prev"] + lambda_ * (u + h_prev)
+        H['u_avg_update'] = u
+        H['alpha_update'] = alpha * (clients / H['total_clients'])
+        return result
+
+    serverGradient.__doc__ = make_server_gradient_frecon.__doc__
+    return serverGradient
+
+
+class _ResponseView:
+    """A Buffer-shaped view over precomputed client vectors (already waited for)."""
+
+    def __init__(self, rows, weights):
+        self.rows, self.weights = rows, weights
+
+    def waitForItem(self):
+        pass
+
+    def get(self, i):
+        return {"model": self.rows[i], "client_state": {"weight": self.weights[i]}}
+
+
 def serverGradientCOFIG(clients_responses, clients, model, params_current, H):
     """COFIG.serverGradient (algorithms.py:1273-1307): the fold u = gs, returned as u + H['h_prev'];
     H['u_avg_update'] = u and H['alpha_update'] = alpha * (clients / H['total_clients']) with alpha

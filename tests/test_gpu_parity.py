@@ -383,3 +383,72 @@ def test_shifted_server_gradients(ag, name):
     assert_bitexact(out, (gs_ref + h).cpu().numpy())
     assert_bitexact(H["u_avg_update"], gs_ref.cpu().numpy())
     assert H["alpha_update"] == 0.37 * (len(items) / 10)
+
+
+def _ref_fold_cpu(x, rows, weights):
+    """algorithms.py:1753-1768 on CPU tensors (true fp32 division by the Python-float total)."""
+    gs = weights[0] * (x - rows[0])
+    tot = weights[0]
+    for w, r in zip(weights[1:], rows[1:]):
+        tot += w
+        gs += w * (x - r)
+    return gs / tot
+
+
+def test_gradskip_and_frecon_server_gradients(ag):
+    """GradSkip (algorithms.py:951-998) and FRECON (1124-1176) wrappers against the reference's
+    bodies restated on CPU tensors."""
+    import types
+
+    class Buf:
+        def __init__(self, items):
+            self.items = items
+
+        def waitForItem(self):
+            pass
+
+        def get(self, i):
+            return self.items[i]
+    g = np.random.default_rng(0)
+    n, d = 5, 4099
+    x = g.standard_normal(d).astype(np.float32)
+    models = [g.standard_normal(d).astype(np.float32) for _ in range(n)]
+    his = [g.standard_normal(d).astype(np.float32) for _ in range(n)]
+    w = [1.0, 0.5, 2.0, 1.5, 1.0]
+    # GradSkip
+    gamma, p = 0.1, 0.5
+    items = [{"model": torch.from_numpy(m).cuda(), "client_state": {
+        "weight": w[i], "local_steps": [], "Ki": 3, "change_shift": i % 2 == 0, "hi": torch.from_numpy(his[i]).cuda(),
+        "grad": torch.from_numpy(his[(i + 1) % n]).cuda(), "stats": {"send_scalars_to_master": 0}}} for i, m in enumerate(models)]
+    H = {"fl_dtype": torch.float32, "args": types.SimpleNamespace(local_lr=gamma), "p": p}
+    out = ag.serverGradientGradSkip(Buf(items), n, None, torch.from_numpy(x).cuda(), H)
+    hi_ref = [his[(i + 1) % n] if i % 2 == 0 else his[i] for i in range(n)]
+    rows = [torch.from_numpy(models[i]) - torch.from_numpy(hi_ref[i]) * gamma / p for i in range(n)]
+    want = _ref_fold_cpu(torch.from_numpy(x), rows, w)
+    assert_bitexact(out, want.numpy())
+    for i in range(n):
+        assert items[i]["client_state"]["local_steps"] == [3 + (1 if i % 2 == 0 else 0)]
+        assert_bitexact(items[i]["client_state"]["delta_x"], (torch.from_numpy(x) - want - torch.from_numpy(models[i])).numpy())
+    # FRECON with the lambda_ experiment option
+    qs = [g.standard_normal(d).astype(np.float32) for _ in range(n)]
+    items = [{"model": torch.from_numpy(m).cuda(), "client_state": {"weight": w[i], "alpha": 0.25,
+                                                                   "qi": torch.from_numpy(qs[i]).cuda()}}
+             for i, m in enumerate(models)]
+    am = types.SimpleNamespace(has_experiment_option=lambda H, k: k == "lambda_",
+                               get_experiment_option_f=lambda H, k: 0.3)
+    gprev = g.standard_normal(d).astype(np.float32)
+    hprev = g.standard_normal(d).astype(np.float32)
+    H = {"fl_dtype": torch.float32, "h_prev": torch.from_numpy(hprev).cuda(), "g_server_prev": torch.from_numpy(gprev).cuda(),
+         "total_clients": 20}
+    out = ag.make_server_gradient_frecon(am)(Buf(items), n, None, torch.from_numpy(x).cuda(), H)
+    u = _ref_fold_cpu(torch.from_numpy(x), [torch.from_numpy(m) for m in models], w)
+    q = w[0] * torch.from_numpy(qs[0])
+    tot = w[0]
+    for wi, qi in zip(w[1:], qs[1:]):
+        tot += wi
+        q += wi * torch.from_numpy(qi)
+    q = q / tot
+    want = q + (1.0 - 0.3) * torch.from_numpy(gprev) + 0.3 * (u + torch.from_numpy(hprev))
+    assert_bitexact(out, want.numpy())
+    assert all("qi" not in it["client_state"] for it in items)
+    assert H["alpha_update"] == 0.25 * (n / 20)

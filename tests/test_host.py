@@ -159,7 +159,7 @@ def test_c_client_of_the_abi(tmp_path):
 def test_install_rebinds_every_shared_fold():
     """install() rebinds the reference classes whose serverGradient is the shared fold
     (algorithms.py: FedAvg, FedProx, MARINA, PP-MARINA, SCAFFOLD plain; DCGD, EF21, EF21PP with the
-    master compressor; DIANA, COFIG shifted) and restores them."""
+    master compressor; DIANA, COFIG, GradSkip, FRECON with their own tails) and restores them."""
     import types
     names = ["FedAvg", "FedProx", "MarinaAlgorithm", "MarinaAlgorithmPP", "SCAFFOLD", "DCGD", "EF21", "EF21PP",
              "DIANA", "COFIG", "GradSkip", "FRECON"]
@@ -179,8 +179,10 @@ def test_install_rebinds_every_shared_fold():
         fn = getattr(algos, n).serverGradient
         if n in want:
             assert fn is want[n], n
+        elif n == "FRECON":
+            assert fn is not orig[n] and "FRECON" in fn.__doc__
         else:
-            assert fn is orig[n], n                     # GradSkip / FRECON keep the reference's
+            assert fn is orig[n], n
     restore()
     for n in names:
         assert getattr(algos, n).serverGradient is orig[n]
