@@ -326,6 +326,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
+        # one node (the bench contract): RCCL's bootstrap on loopback unless the caller chose
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("nccl", device_id=dev)
 
     from flpytorch_amd import _lib

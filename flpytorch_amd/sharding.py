@@ -70,3 +70,66 @@ def product_partial(reducer):
     def run(rows, client0, out):
         reducer(rows, out=out, client0=client0, divisor=1.0)
     return run
+
+
+# ---------------------------------------------------------------------------------------------
+# The C-ABI combine (flc_combine_partials) on a caller-owned RCCL communicator: the path a non-torch
+# host (the C ABI's own callers) takes; torch.distributed's communicator stays private to torch.
+# ---------------------------------------------------------------------------------------------
+class RcclComm:
+    """A caller-owned RCCL communicator over the ranks of a torch.distributed group (any backend:
+    the 128-byte unique id travels through it), one GPU per rank."""
+
+    def __init__(self, group=None):
+        import ctypes
+        import os
+        # one node: RCCL's bootstrap on the loopback interface unless the caller chose one
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        self._ct = ctypes
+        self.lib = ctypes.CDLL("librccl.so")
+
+        class UniqueId(ctypes.Structure):
+            _fields_ = [("internal", ctypes.c_char * 128)]
+        self._uid_t = UniqueId
+        self.lib.ncclGetUniqueId.argtypes = [ctypes.POINTER(UniqueId)]
+        self.lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, UniqueId, ctypes.c_int]
+        self.lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        rank = dist.get_rank(group)
+        world = dist.get_world_size(group)
+        uid = UniqueId()
+        if rank == 0:
+            if self.lib.ncclGetUniqueId(ctypes.byref(uid)) != 0:
+                raise RuntimeError("ncclGetUniqueId failed")
+        # the raw 128 bytes (a c_char array field reads back only up to its first NUL)
+        box = [ctypes.string_at(ctypes.addressof(uid), 128) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        ctypes.memmove(ctypes.addressof(uid), box[0], 128)
+        self.ptr = ctypes.c_void_p()
+        rc = self.lib.ncclCommInitRank(ctypes.byref(self.ptr), world, uid, rank)
+        if rc != 0:
+            self.lib.ncclGetErrorString.restype = ctypes.c_char_p
+            raise RuntimeError(f"ncclCommInitRank failed: {rc} {self.lib.ncclGetErrorString(rc).decode()}")
+        self.world = world
+
+    def destroy(self):
+        if self.ptr:
+            self.lib.ncclCommDestroy(self.ptr)
+            self.ptr = self._ct.c_void_p()
+
+
+def combine_partials(comm, partial, total_weight, ordered=False):
+    """In place: partial <- (sum over ranks of partial) / total_weight through flc_combine_partials
+    (FLC_COMBINE_ORDERED: fixed rank-order fold, bit-reproducible)."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    mode = 1 if ordered else 0
+    d = partial.numel()
+    ws_bytes = lib.flc_combine_workspace_size(comm.ptr, d, mode)
+    ws = _lib.WORKSPACE.get(partial.device, ws_bytes) if ws_bytes else None
+    with torch.cuda.device(partial.device):
+        rc = lib.flc_combine_partials(comm.ptr, ctypes.c_void_p(partial.data_ptr()), d, ctypes.c_float(float(total_weight)),
+                                      mode, ctypes.c_void_p(ws.data_ptr() if ws is not None else None),
+                                      ws.numel() if ws is not None else 0, _lib.stream_ptr(partial.device))
+    _lib.check(rc, "flc_combine_partials")
+    return partial

@@ -192,6 +192,22 @@ int flc_unpack_reduce(const flc_codec_params* prm, const void* d_payloads, int64
                       float w_total, float* d_out, void* d_ws, size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------------------------------------
+ * Multi-GPU combine on a caller-owned RCCL communicator (rccl_comm: an ncclComm_t, passed as
+ * void* so no RCCL type crosses the boundary).  Each rank's d_partial holds the client-order
+ * partial sum of its client block (flc_encode_reduce / flc_unpack_reduce with w_total = 1.0);
+ * on return every rank holds the global result:
+ *   FLC_COMBINE_ALLREDUCE  in-place all-reduce(sum), then / w_total (RCCL's summation order)
+ *   FLC_COMBINE_ORDERED    all-gather into d_ws, fixed rank-order fold, / w_total
+ *                          (bit-reproducible; d_ws of flc_combine_workspace_size bytes)
+ * Replaces the reference's per-client .to(device) gathering into one master thread
+ * (thread_pool.py:59, algorithms.py:1756-1763).  Enqueued on stream; no host synchronisation.
+ * -------------------------------------------------------------------------------------- */
+enum { FLC_COMBINE_ALLREDUCE = 0, FLC_COMBINE_ORDERED = 1 };
+size_t flc_combine_workspace_size(void* rccl_comm, int64_t d, int mode);
+int flc_combine_partials(void* rccl_comm, float* d_partial, int64_t d, float w_total, int mode,
+                         void* d_ws, size_t ws_bytes, void* stream);
+
+/* ----------------------------------------------------------------------------------------
  * Host side of compat mode: the numpy legacy MT19937 stream (what the reference's
  * rndgen.choice / rand / random / randint draw, compressors.py:204-212, algorithms.py:2055),
  * advanced in place on a caller-held state (key[624], pos — numpy's get_state() layout).
