@@ -1,0 +1,63 @@
+"""SURVEY §8b threading contract: the library is reentrant across host threads that use distinct
+streams (the reference's worker threads call compressVector concurrently, worker_thread.py:60-64).
+Eight threads, each on its own HIP stream, run every codec family at once; every result equals the
+same call made alone."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SPECS = ["topk:1%", "qsgd:127", "randk:1%", "natural", "std.dithering:8:2", "rank_k:4", "qsgd:16", "ident"]
+
+
+def test_concurrent_threads_distinct_streams():
+    assert torch.cuda.is_available()
+    from flpytorch_amd import aggregation as ag
+    n, d = 6, 200003
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rows = [torch.randn(n, d, generator=g, device="cuda") for _ in SPECS]
+
+    def run(i, stream=None):
+        red = ag.UplinkReducer(ag.initCompressor(SPECS[i], d), seed=100 + i)
+        if stream is None:
+            return red(rows[i]).clone()
+        with torch.cuda.stream(stream):
+            out = red(rows[i], stream=stream)
+            c = ag.initCompressor(SPECS[i], d)
+            c.device_rng = (100 + i, 0)
+            one = c.compressVector(rows[i][0])
+        stream.synchronize()
+        return out.clone(), one.clone()
+
+    want = [run(i) for i in range(len(SPECS))]
+    want_one = []
+    for i in range(len(SPECS)):
+        c = ag.initCompressor(SPECS[i], d)
+        c.device_rng = (100 + i, 0)
+        want_one.append(c.compressVector(rows[i][0]).clone())
+    torch.cuda.synchronize()
+    got, errors = [None] * len(SPECS), []
+
+    def worker(i):
+        try:
+            s = torch.cuda.Stream()
+            for _ in range(3):
+                got[i] = run(i, s)
+        except Exception as e:          # surfaced below
+            errors.append((i, repr(e)))
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(len(SPECS))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    for i, spec in enumerate(SPECS):
+        out, one = got[i]
+        if spec.startswith("rank_k"):
+            assert (out - want[i]).norm().item() <= 1e-5 * (1 + want[i].norm().item())
+        else:
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want[i].cpu().numpy().view(np.uint32)), spec
+            assert np.array_equal(one.cpu().numpy().view(np.uint32), want_one[i].cpu().numpy().view(np.uint32)), spec
