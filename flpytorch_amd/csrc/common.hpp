@@ -104,6 +104,15 @@ int sel_unpack_reduce(const flc_codec_params* prm, const void* base, int64_t ld_
                       hipStream_t st);
 size_t sel_unpack_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int64_t payload_bytes(const flc_codec_params* prm, int64_t d);
+int64_t rk_payload_floats(const flc_codec_params* prm, int64_t d);
+int64_t rk_rank(const flc_codec_params* prm, int64_t d);
+int rk_pack(const flc_codec_params* prm, const float* x, int64_t d, float* body, void* wsp, size_t ws_bytes,
+            hipStream_t st);
+size_t rk_unpack_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
+int rk_unpack1(const flc_codec_params* prm, const float* body, int64_t d, float* out, hipStream_t st);
+int rk_unpack_reduce(const flc_codec_params* prm, const char* base, int64_t ld, const char* const* ptrs, int64_t n,
+                     int64_t d, const float* w, float wt, float* out, bool reduce, void* wsp, size_t ws_bytes,
+                     hipStream_t st);
 int payload_format(const flc_codec_params* prm);
 size_t pack_workspace(const flc_codec_params* prm, int64_t d);
 int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, char* payload, void* ws,

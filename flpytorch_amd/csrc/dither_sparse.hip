@@ -668,6 +668,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         if (probe == 2) launch(k_ds_filter<16, DS_GCAP, 2>);
         else if (probe == 3) launch(k_ds_filter<16, DS_GCAP, 3>);
         else if (probe == 4) launch(k_ds_filter<16, DS_GCAP, 4>);
+        else if (probe == 5) launch(k_ds_filter<16, DS_GCAP, 5>);
         else if (v.fgs == 4 && v.gcap == 1024) launch(k_ds_filter<16, 1024, 0, 4>);
         else if (v.fgs == 4) launch(k_ds_filter<16, DS_GCAP, 0, 4>);
         else if (v.gcap == 1024) launch(k_ds_filter<16, 1024>);

@@ -4,13 +4,15 @@
 // dense decoded tensor; comm_socket.py pickles that).
 //
 // One row's payload: a 16-B header {u32 format, u32 count, f32 norm, u32 d} and a body, 16-B padded:
-//   F32     ident / lazy / natural dithering (the reference's output is ~x) / rank_k: f32[d]
+//   F32     ident / lazy / natural dithering (the reference's output is ~x): f32[d]
 //   Q8      standard dithering / QSGD / TernGrad, s <= 127: u8[d]   bit 7 sign, bits 0-6 level index
 //   Q16     standard dithering, 127 < s <= 32767:         u16[d]  bit 15 sign, bits 0-14 level index
 //   NAT16   natural:                                       u16[d]  bit 15 sign, bits 0-14: 0 zero,
 //           0x7FFE inf, 0x7FFF NaN, else k + 16384 for the value 2^k (k in [-149, 127])
 //   SPARSE  randk / topk: count (<= K) entries, u32 idx[K] then f32 val[K], ascending idx; the
 //           entries are the output's elements whose bits are not +0
+//   RANKK   rank_k: the factor block of rank_k.hip — U'_K (B x K) then (S V'^T)_K (K x A), f32,
+//           K' (A + B) values as the reference counts them (compressors.py:362)
 // Level codes: value = (levels[idx] * sign) * norm exactly as the encode (compressors.py:294-296);
 // code 0 is +0 exactly (x == 0), sign + level 0 with the sign bit is -0 * norm (NaN when the norm is
 // not finite).  Decoding a payload gives the dense compressVector output bit for bit
@@ -25,7 +27,7 @@
 
 namespace flc {
 
-enum { FMT_F32 = 1, FMT_Q8 = 2, FMT_Q16 = 3, FMT_NAT16 = 4, FMT_SPARSE = 5 };
+enum { FMT_F32 = 1, FMT_Q8 = 2, FMT_Q16 = 3, FMT_NAT16 = 4, FMT_SPARSE = 5, FMT_RANKK = 6 };
 struct PayloadHeader {
     uint32_t fmt, count;
     float norm;
@@ -40,6 +42,7 @@ int payload_format(const flc_codec_params* prm) {
         case FLC_NATURAL: return FMT_NAT16;
         case FLC_RANDK:
         case FLC_TOPK: return FMT_SPARSE;
+        case FLC_RANK_K: return FMT_RANKK;
         default: return FMT_F32;
     }
 }
@@ -50,6 +53,7 @@ int64_t payload_bytes(const flc_codec_params* prm, int64_t d) {
         case FMT_Q16:
         case FMT_NAT16: return 16 + a16(2 * d);
         case FMT_SPARSE: { const int64_t k = std::max<int64_t>(1, std::min(prm->k, d)); return 16 + 2 * a16(4 * k); }
+        case FMT_RANKK: return 16 + a16(4 * rk_payload_floats(prm, d));
         default: return 16 + a16(4 * d);
     }
 }
@@ -109,6 +113,17 @@ __device__ inline float nat_decode(uint32_t c) {
 }
 
 // ---- pack ---------------------------------------------------------------------------------------
+__global__ void k_rankk_header(char* payload, uint32_t floats, uint32_t k) {
+    if (threadIdx.x == 0) {
+        PayloadHeader* h = reinterpret_cast<PayloadHeader*>(payload);
+        h->fmt = FMT_RANKK;
+        h->count = k;          // rank of the expansion (K' = min(K, A, B) factors are stored)
+        h->norm = 0.f;
+        h->bad = 0u;
+        (void)floats;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_pack_dense(const float* __restrict__ v, int64_t d, int fmt,
                                                     const float* __restrict__ levels, int s,
                                                     const float* __restrict__ pnorm, char* __restrict__ payload) {
@@ -344,6 +359,7 @@ static PackWs carve_pack(void* base, const flc_codec_params* prm, int64_t d, siz
 }
 
 size_t pack_workspace(const flc_codec_params* prm, int64_t d) {
+    if (payload_format(prm) == FMT_RANKK) return rk_workspace(prm, 1, d, false);
     size_t b = 0;
     carve_pack(nullptr, prm, d, &b);
     return b;
@@ -355,8 +371,17 @@ int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x
              size_t ws_bytes, hipStream_t st) {
     if (ws_bytes < pack_workspace(prm, d)) { set_error("flc_pack: workspace too small"); return FLC_ERR_WORKSPACE; }
     if ((uintptr_t)payload & 15u) { set_error("flc_pack: payload must be 16-byte aligned"); return FLC_ERR_ARG; }
-    PackWs w = carve_pack(ws, prm, d, nullptr);
     const int fmt = payload_format(prm);
+    if (fmt == FMT_RANKK) {
+        const int64_t pb = payload_bytes(prm, d);
+        FLC_CHECK_HIP(hipMemsetAsync(payload, 0, (size_t)pb, st));
+        if (d == 0) return FLC_OK;
+        hipLaunchKernelGGL(k_rankk_header, dim3(1), dim3(64), 0, st, payload, (uint32_t)rk_payload_floats(prm, d),
+                           (uint32_t)rk_rank(prm, d));
+        FLC_CHECK_LAUNCH("k_rankk_header");
+        return rk_pack(prm, x, d, reinterpret_cast<float*>(payload + 16), ws, ws_bytes, st);
+    }
+    PackWs w = carve_pack(ws, prm, d, nullptr);
     // header zeroed; the body's 16-B padding (and the unused part of a sparse list) zeroed too, so
     // a payload's bytes are a function of the row alone
     const int64_t pb = payload_bytes(prm, d);
@@ -396,6 +421,7 @@ int unpack_run(const flc_codec_params* prm, const char* payload, int64_t d, floa
     if (d == 0) return FLC_OK;
     if ((uintptr_t)payload & 15u) { set_error("flc_unpack: payload must be 16-byte aligned"); return FLC_ERR_ARG; }
     const int fmt = payload_format(prm);
+    if (fmt == FMT_RANKK) return rk_unpack1(prm, reinterpret_cast<const float*>(payload + 16), d, out, st);
     if (fmt == FMT_SPARSE) {
         const int64_t cap = std::max<int64_t>(1, std::min(prm->k, d));
         FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
@@ -411,6 +437,7 @@ int unpack_run(const flc_codec_params* prm, const char* payload, int64_t d, floa
 }
 
 size_t unpack_reduce_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
+    if (payload_format(prm) == FMT_RANKK) return rk_unpack_workspace(prm, n, d);
     return payload_format(prm) == FMT_SPARSE ? sel_unpack_workspace(prm, n, d) : 0;
 }
 
@@ -420,6 +447,7 @@ int unpack_reduce_run(const flc_codec_params* prm, const char* base, int64_t ld,
     if (n == 0) { FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st)); return FLC_OK; }
     const int fmt = payload_format(prm);
     if (fmt == FMT_SPARSE) return sel_unpack_reduce(prm, base, ld, (const void* const*)ptrs, n, d, w, wt, out, ws, ws_bytes, st);
+    if (fmt == FMT_RANKK) return rk_unpack_reduce(prm, base, ld, ptrs, n, d, w, wt, out, /*reduce=*/true, ws, ws_bytes, st);
     if (base && ((ld & 15) || ((uintptr_t)base & 15u))) { set_error("flc_unpack_reduce: payload rows must be 16-byte aligned"); return FLC_ERR_ARG; }
     const int E = fmt == FMT_Q8 ? 16 : (fmt == FMT_F32 ? 4 : 8);
     const int64_t groups = d / E + 1;

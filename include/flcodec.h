@@ -165,13 +165,17 @@ int flc_encode_shift(const flc_codec_params* prm, const flc_pattern* pat, const 
  * (last_need_to_send_advance, compressors.py:223-224, 367-368) but moves the dense decoded
  * tensor (comm_socket.py:16-82 pickles it).  One row's payload = 16-B header
  * {u32 format, u32 count, f32 norm, u32 bad} + body, padded to 16 B:
- *   1 F32    ident, lazy, natural dithering, rank_k        f32[d]
+ *   1 F32    ident, lazy, natural dithering                f32[d]
  *   2 Q8     std dithering / qsgd / terngrad, s <= 127     u8[d]: bit 7 sign, bits 0-6 level index
  *   3 Q16    std dithering, s > 127                        u16[d]: bit 15 sign, bits 0-14 level index
  *   4 NAT16  natural                                       u16[d]: bit 15 sign; 0 zero, 0x7FFE inf,
  *                                                          0x7FFF NaN, else k + 16384 for 2^k
  *   5 SPARSE randk, topk                                   u32 idx[K] then f32 val[K] (count used,
  *                                                          ascending idx, the elements not +0)
+ *   6 RANKK  rank_k                                        the rank-K' expansion, f32: U'_K (B x K')
+ *                                                          then (S V'^T)_K' (K' x A), each 16-B
+ *                                                          padded — K' (A + B) values, count = K'
+ *                                                          (decoded by the encode's own GEMM)
  * Level code 0 is +0; otherwise value = (levels[idx] * sign) * norm (compressors.py:294-296).
  * flc_unpack(flc_pack(x)) == flc_encode(x) bit for bit; flc_unpack_reduce(payloads) ==
  * flc_encode_reduce(rows).  flc_pack runs the encode (same patterns and draws as flc_encode)

@@ -9,7 +9,7 @@ import numpy as np
 
 from oracle import codecs as oc
 
-F32, Q8, Q16, NAT16, SPARSE = 1, 2, 3, 4, 5
+F32, Q8, Q16, NAT16, SPARSE, RANKK = 1, 2, 3, 4, 5, 6
 _F = np.float32
 
 
@@ -24,6 +24,8 @@ def payload_format(comp):
         return NAT16
     if comp.type in (oc.RANDK, oc.TOPK):
         return SPARSE
+    if comp.type == oc.RANK_K:
+        return RANKK
     return F32
 
 
@@ -36,6 +38,9 @@ def payload_bytes(comp, d):
     if f == SPARSE:
         k = max(1, min(comp.K, d))
         return 16 + 2 * _a16(4 * k)
+    if f == RANKK:                       # U'_K (B x K') and (S V'^T)_K' (K' x A), 16-B padded each
+        k = min(comp.K, comp.A, comp.B)
+        return 16 + _a16(4 * (((comp.B * k + 3) & ~3) + ((k * comp.A + 3) & ~3)))
     return 16 + _a16(4 * d)
 
 
@@ -105,6 +110,8 @@ def pack(comp, out, pnorm=None):
     out = np.asarray(out, dtype=_F)
     d = out.size
     f = payload_format(comp)
+    if f == RANKK:
+        raise NotImplementedError("rank_k payloads hold the SVD factors; their signs are the solver's own")
     buf = np.zeros(payload_bytes(comp, d), dtype=np.uint8)
     hdr = np.zeros(4, dtype=np.uint32)
     hdr[0] = f

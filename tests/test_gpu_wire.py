@@ -109,3 +109,27 @@ def test_payload_sizes(ag):
     assert ag.initCompressor("qsgd:127", d).payloadBytes() == 16 + d            # 1 byte per element
     assert ag.initCompressor("topk:1%", d).payloadBytes() == 16 + 8 * 250000
     assert ag.initCompressor("natural", d).payloadBytes() == 16 + 2 * d
+
+
+@pytest.mark.parametrize("spec,d", [("rank_k:3", 2465), ("rank_k:8", 65536), ("rank_k:50", 12), ("rank_k:4", 97)])
+def test_rank_k_payload(ag, spec, d):
+    """Rank-K messages are the K' (A + B) factor values (compressors.py:362): decode == the encode bit
+    for bit (one GEMM shape), the server fold from payloads == the fused uplink to fp32 rounding."""
+    g = torch.Generator(device="cuda").manual_seed(d)
+    rows = torch.randn(4, d, generator=g, device="cuda")
+    comp = ag.initCompressor(spec, d)
+    k = min(comp.K, comp.A, comp.B)
+    assert comp.payloadBytes() == wire.payload_bytes(oc.OracleCompressor(spec, d), d)
+    assert comp.payloadBytes() >= 16 + 4 * k * (comp.A + comp.B)
+    pls = [comp.compressPayload(rows[i]) for i in range(4)]
+    assert comp.last_need_to_send_advance == k * (comp.A + comp.B)
+    hdr = pls[0][:16].cpu().numpy().view(np.uint32)
+    assert hdr[0] == 6 and hdr[1] == k
+    for i in range(4):
+        dec = comp.decompressPayload(pls[i], d)
+        assert np.array_equal(bits(dec), bits(ag.initCompressor(spec, d).compressVector(rows[i])))
+    got = ag.PayloadReducer(comp)(torch.stack(pls), d=d)
+    want = ag.UplinkReducer(ag.initCompressor(spec, d))(rows)
+    assert (got - want).norm().item() <= 1e-6 * (1.0 + want.norm().item())
+    got2 = ag.PayloadReducer(comp)(pls, d=d)
+    assert np.array_equal(bits(got), bits(got2))
