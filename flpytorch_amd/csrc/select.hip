@@ -1204,8 +1204,9 @@ static int grid_stride_blocks(int64_t items, int64_t cap = 4096) {
 // Runs the TopK / RandK pipeline for n rows and writes out (ASSIGN: n == 1 dense encode).
 static int accum_parts() {
     static const int p = [] {
-        const char* e = getenv("FLC_ACCUM_PARTS");   // tuning runs only
-        return (e && atoi(e) == 1) ? 1 : (e && atoi(e) == 2) ? 2 : 1;
+        const char* e = getenv("FLC_ACCUM_PARTS");   // tuning runs only (0 / unset: by chunk count)
+        const int v = e ? atoi(e) : 0;
+        return (v == 1 || v == 2 || v == 4) ? v : 0;
     }();
     return p;
 }
@@ -1317,7 +1318,15 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
     { ProfScope _ps("k_chunk_accum", st);
-    if (accum_parts() == 2) {
+    // few chunks (short rows: C2's D = 1 M has 245): split each chunk's columns over 2 or 4 waves so
+    // the latency-bound row walk runs on more of the chip (many chunks: one wave each, measured best)
+    int parts = accum_parts();
+    if (parts == 0) parts = C >= 1024 ? 1 : (C >= 256 ? 2 : 4);
+    if (parts == 4) {
+        const int ab = grid_stride_blocks((4 * C + 3) / 4, 8192);
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    } else if (parts == 2) {
         const int ab = grid_stride_blocks((2 * C + 3) / 4, 8192);
         if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
         else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
