@@ -290,6 +290,51 @@ def e2e_wire(args):
                       "note": "payloads in pinned host memory; 2-stream H2D/fold overlap, blocks of 8 clients"}))
 
 
+def dropin(args):
+    """The drop-in path as the reference's algorithms drive it after install(): every client's
+    Compressor.compressVector (generateCompressPattern on the caller's numpy stream first: compat
+    mode, the reference's own draws) and then the serverGradient fold of the N dense outputs
+    (reduce_rows) — against the fused uplink (UplinkReducer) on the same rows.  Own line, not value."""
+    from flpytorch_amd import aggregation as ag
+    wl = dict(WORKLOADS[args.workload])
+    n = args.n or 32
+    d = args.d or wl["d"]
+    spec = wl["spec"] if wl["spec"] != "mixed" else "qsgd:127"
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    gen = torch.Generator(device=dev).manual_seed(9)
+    rows = torch.randn(n, d, generator=gen, device=dev)
+    x = torch.zeros(d, device=dev)
+    comps = [ag.initCompressor(spec, d) for _ in range(n)]
+    rs = np.random.RandomState(123)
+
+    def per_client(patterns=True):
+        outs = []
+        for i in range(n):
+            if patterns:
+                comps[i].generateCompressPattern(rs, "cuda", i, {})
+            outs.append(comps[i].compressVector(rows[i]))
+        return ag.reduce_rows(x, outs, relative=False)
+
+    red = ag.UplinkReducer(ag.initCompressor(spec, d), device=dev, seed=5)
+    res = {}
+    for name, fn in [("per_client_compat_incl_patterns", lambda: per_client(True)),
+                     ("per_client_encode_and_fold_only", lambda: per_client(False)),
+                     ("fused_uplink_device_rng", lambda: red(rows))]:
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
+    print(json.dumps({"mode": "drop-in path (compressVector per client + serverGradient fold) vs fused uplink",
+                      "codec": spec, "clients": n, "D": d, "ms_per_round": res,
+                      "note": "compat mode draws the reference's numpy stream on the host (MT19937 in C++) "
+                              "and uploads it; the second line reuses the drawn patterns"}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -299,12 +344,16 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dropin", action="store_true",
+                    help="per-client compressVector + serverGradient fold (the install() path) vs the fused uplink")
     ap.add_argument("--wire", action="store_true",
                     help="server side from the wire format: decode+reduce of N resident payloads (own line, not value)")
     ap.add_argument("--e2e", action="store_true",
                     help="end-to-end: client rows start in pinned host memory, the [D] result lands in host memory "
                          "(H2D + encode+reduce + D2H per step; PCIe-bound; reported in DESIGN.md, never as value)")
     args = ap.parse_args()
+    if args.dropin:
+        return dropin(args)
     if args.e2e and args.wire:
         return e2e_wire(args)
     if args.e2e:

@@ -14,6 +14,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "../../include/flcodec.h"
@@ -103,7 +105,45 @@ extern "C" int flc_mt_rand(uint32_t* h_key, int32_t* h_pos, int64_t n, double* h
         return FLC_ERR_ARG;
     }
     Mt mt{h_key, h_pos, 0};
-    for (int64_t i = 0; i < n; ++i) h_out[i] = mt.next_double();
+    int64_t i = 0;
+    // a pair straddling the end of the 624-word block: the scalar path
+    while (i < n && (*h_pos & 1) && *h_pos < 624) h_out[i++] = mt.next_double();
+    if (i == n) return FLC_OK;
+    // 1) sequential: the raw (untempered) words of the remaining draws, block by block, parked in
+    //    the output array itself (a pair of words occupies exactly the 8 bytes of its double);
+    uint32_t* raw = reinterpret_cast<uint32_t*>(h_out + i);
+    const int64_t m_total = n - i;
+    int64_t w = 0;
+    while (w < 2 * m_total) {
+        if (*h_pos >= 624) mt.twist();
+        const int64_t take = std::min<int64_t>(624 - *h_pos, 2 * m_total - w);
+        memcpy(raw + w, h_key + *h_pos, (size_t)take * sizeof(uint32_t));
+        *h_pos += (int32_t)take;
+        w += take;
+    }
+    // 2) parallel, in place: tempering and the 53-bit conversion (a * 2^26 + b) * 2^-53 (the
+    //    reference's division by 2^53 is exact, so is the product)
+    auto convert = [raw](int64_t t0, int64_t t1) {
+        double* o = reinterpret_cast<double*>(raw);
+        for (int64_t t = t0; t < t1; ++t) {
+            uint32_t a = raw[2 * t], b = raw[2 * t + 1];
+            a ^= (a >> 11); a ^= (a << 7) & 0x9d2c5680u; a ^= (a << 15) & 0xefc60000u; a ^= (a >> 18);
+            b ^= (b >> 11); b ^= (b << 7) & 0x9d2c5680u; b ^= (b << 15) & 0xefc60000u; b ^= (b >> 18);
+            o[t] = ((double)(int32_t)(a >> 5) * 67108864.0 + (double)(int32_t)(b >> 6)) * (1.0 / 9007199254740992.0);
+        }
+    };
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int64_t per = (m_total + hw - 1) / hw;
+    if (hw == 1 || m_total < (1 << 18)) {
+        convert(0, m_total);
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned q = 0; q < hw; ++q) {
+            const int64_t t0 = (int64_t)q * per, t1 = std::min<int64_t>(m_total, t0 + per);
+            if (t0 < t1) th.emplace_back(convert, t0, t1);
+        }
+        for (auto& t : th) t.join();
+    }
     return FLC_OK;
 }
 
