@@ -25,7 +25,15 @@ namespace flc {
 // p-norms: partial[row][part] (float64, fixed slots) then one wave per row folds them in a
 // fixed order -> deterministic, exactly rounded fp32 norm.
 // ------------------------------------------------------------------------------------------
-constexpr int NORM_PART = 65536;   // elements per partial (256 threads x 64 elements)
+constexpr int NORM_PART = 65536;   // elements per partial (256 threads x 64 elements) ...
+constexpr int NORM_PART_MIN = 4096; // ... halved for few rows so a short launch still spans the chip
+
+// elements per partial for n rows of d: 65536, halved (down to 4096) while n * parts < 2048
+int64_t norm_part_len(int64_t n, int64_t d) {
+    int64_t len = NORM_PART;
+    while (len > NORM_PART_MIN && std::max<int64_t>(n, 1) * ((d + len - 1) / len) < 2048) len >>= 1;
+    return len;
+}
 
 template <int NORM>
 __device__ inline double nacc(double a, float v) {
@@ -45,7 +53,7 @@ __device__ inline uint32_t is_tiny(float v) { const float a = fabsf(v); return (
 // DIFF: the row is the fp32 difference src.row(0) - sub (the shift codecs' C(a - b), one row)
 template <int NORM, bool VEC, bool DIFF>
 __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, const float* __restrict__ sub, int64_t d,
-                                                       int64_t parts, double* __restrict__ partial,
+                                                       int64_t parts, int64_t plen, double* __restrict__ partial,
                                                        uint32_t* __restrict__ tinyp) {
     const int64_t row = blockIdx.y;
     const float* r = src.row(row);
@@ -53,12 +61,12 @@ __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, const float* 
     __shared__ double red[4];
     __shared__ uint32_t redt[4];
     for (int64_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        const int64_t j0 = part * NORM_PART;
-        const int64_t j1 = min(d, j0 + (int64_t)NORM_PART);
+        const int64_t j0 = part * plen;
+        const int64_t j1 = min(d, j0 + plen);
         double a = 0.0;
         uint32_t tiny = 0;
         if (VEC) {
-            const int64_t g0 = j0 / 4, g1 = j1 / 4;   // j0 % 4 == 0 (NORM_PART % 4 == 0)
+            const int64_t g0 = j0 / 4, g1 = j1 / 4;   // j0 % 4 == 0 (plen % 4 == 0)
             for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
                 float4 v = reinterpret_cast<const float4*>(r)[g];
                 if (DIFF) {
@@ -118,13 +126,13 @@ __global__ __launch_bounds__(64) void k_norm_final(const double* __restrict__ pa
     }
 }
 
-int64_t norm_parts(int64_t d) { return (d + NORM_PART - 1) / NORM_PART; }
+int64_t norm_parts(int64_t n, int64_t d) { const int64_t l = norm_part_len(n, d); return (d + l - 1) / l; }
 
 int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* partial, uint32_t* tinyp,
                  float* pn, float* rpn, uint32_t* rowfast, uint64_t seed, int64_t client0, uint32_t* rk,
                  hipStream_t st, const float* sub) {
     if (sub && n != 1) { set_error("launch_norms: a difference source is one row"); return FLC_ERR_ARG; }
-    const int64_t parts = norm_parts(d);
+    const int64_t parts = norm_parts(n, d), plen = norm_part_len(n, d);
     if (n == 0) return FLC_OK;
     if (parts == 0) {  // d == 0: norm of an empty vector
         FLC_CHECK_HIP(hipMemsetAsync(pn, 0, (size_t)n * sizeof(float), st));
@@ -132,13 +140,14 @@ int launch_norms(RowSrc src, bool vec, int64_t n, int64_t d, int norm, double* p
         FLC_CHECK_HIP(hipMemsetAsync(rk, 0, (size_t)n * sizeof(uint32_t), st));
         return FLC_OK;
     }
-    dim3 grid((unsigned)std::min<int64_t>(parts, 64), (unsigned)n);
+    // blocks per row: up to 64 for many rows, more when the rows are few (all parts in flight)
+    dim3 grid((unsigned)std::min<int64_t>(parts, std::max<int64_t>(64, 4096 / std::max<int64_t>(n, 1))), (unsigned)n);
 #define FLC_NORM_CASE(NK)                                                                           \
     { ProfScope _ps("k_norm_partials", st);                                                         \
-    if (sub && vec) hipLaunchKernelGGL((k_norm_partials<NK, true, true>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); \
-    else if (sub) hipLaunchKernelGGL((k_norm_partials<NK, false, true>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); \
-    else if (vec) hipLaunchKernelGGL((k_norm_partials<NK, true, false>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); \
-    else hipLaunchKernelGGL((k_norm_partials<NK, false, false>), grid, dim3(256), 0, st, src, sub, d, parts, partial, tinyp); } \
+    if (sub && vec) hipLaunchKernelGGL((k_norm_partials<NK, true, true>), grid, dim3(256), 0, st, src, sub, d, parts, plen, partial, tinyp); \
+    else if (sub) hipLaunchKernelGGL((k_norm_partials<NK, false, true>), grid, dim3(256), 0, st, src, sub, d, parts, plen, partial, tinyp); \
+    else if (vec) hipLaunchKernelGGL((k_norm_partials<NK, true, false>), grid, dim3(256), 0, st, src, sub, d, parts, plen, partial, tinyp); \
+    else hipLaunchKernelGGL((k_norm_partials<NK, false, false>), grid, dim3(256), 0, st, src, sub, d, parts, plen, partial, tinyp); } \
     FLC_CHECK_LAUNCH("k_norm_partials");                                                            \
     hipLaunchKernelGGL((k_norm_final<NK>), dim3((unsigned)n), dim3(64), 0, st, partial, tinyp, parts, n, pn, rpn,   \
                        rowfast, seed, client0, rk);                                                 \
@@ -430,7 +439,7 @@ struct EwWs {
 };
 static EwWs carve_ew(void* base, int64_t n, int64_t d, size_t* bytes) {
     Carver c(base);
-    const size_t np = (size_t)std::max<int64_t>(n, 1), parts = (size_t)std::max<int64_t>(norm_parts(d), 1);
+    const size_t np = (size_t)std::max<int64_t>(n, 1), parts = (size_t)std::max<int64_t>(norm_parts(n, d), 1);
     EwWs w;
     w.partial = c.take<double>(np * parts);
     w.tinyp = c.take<uint32_t>(np * parts);

@@ -124,13 +124,13 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
         const int P = SMAX / 256;
         S = SMAX;
         // piece p = 256 contiguous elements at p (d - 256) / (P - 1); thread t reads element t of
-        // 8 pieces per round trip
-        for (int p0 = 0; p0 < P; p0 += 8) {
-            float x[8];
+        // 32 pieces per round trip (a lone row's sample is latency-bound: few trips)
+        for (int p0 = 0; p0 < P; p0 += 32) {
+            float x[32];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) x[u] = r[((int64_t)(p0 + u) * (d - 256)) / (P - 1) + threadIdx.x];
+            for (int u = 0; u < 32; ++u) x[u] = r[((int64_t)(p0 + u) * (d - 256)) / (P - 1) + threadIdx.x];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) keys[(p0 + u) * 256 + threadIdx.x] = mag_key(x[u]);
+            for (int u = 0; u < 32; ++u) keys[(p0 + u) * 256 + threadIdx.x] = mag_key(x[u]);
         }
     }
     // rank (from the top) of the sample element whose key is the threshold
