@@ -12,8 +12,13 @@
 //                    magnitude is tied ambiguously are redone exactly on the full row
 //                    (3 radix passes + tie prefix + exact filter, ties -> lowest index first)
 //   RandK lists    : per row the K indices (numpy stream, or the device Feistel sampler) are
-//                    bucketed by chunk (count, scan, scatter) with value (D/K)*x[j]
-//   accumulate     : one wave owns one chunk as an fp32 LDS tile and folds the rows' admitted
+//                    bucketed by chunk in two coalesced levels — superchunks in one workgroup
+//                    per row (LDS counts + multi-split), then chunks inside each superchunk (LDS
+//                    counting sort) with the gather of (D/K) * x[j] in ascending order
+//                    (k_randk_coarse / k_randk_fine); a one-level global-atomic path is kept
+//                    behind FLC_RANDK_GLOBAL for A/B runs
+//   accumulate     : one wave owns one chunk (or 1/2, 1/4 of it when the rows are short) as an
+//                    fp32 LDS tile and folds the rows' admitted
 //                    entries in row order -> (sum_i w_i C_i(x_i)) / w_total, bit-identical to the
 //                    sequential reduction of the dense compressVector outputs (indices are
 //                    distinct within a row, so every element sees its terms in row order).
