@@ -63,23 +63,24 @@ struct SelWs {            // carved from the caller workspace
 __device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
                                  uint32_t* scratch /* LDS 256+2 */) {
     const int t = threadIdx.x;
+    const bool own = t < 256;                              // larger blocks: the rest only sync
     // thread t owns bins [HBINS-8(t+1), HBINS-8t)  (top bins first)
     uint32_t local[8];
     uint32_t s = 0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) { local[q] = h[HBINS - 1 - (t * 8 + q)]; s += local[q]; }
+    for (int q = 0; q < 8; ++q) { local[q] = own ? h[HBINS - 1 - (t * 8 + q)] : 0u; s += local[q]; }
     if (t == 0) { scratch[256] = 0; scratch[257] = 0; }   // defined result even if k > total
-    scratch[t] = s;
+    if (own) scratch[t] = s;
     __syncthreads();
     // inclusive scan (Hillis-Steele) over 256 thread sums
     for (int off = 1; off < 256; off <<= 1) {
-        uint32_t v = (t >= off) ? scratch[t - off] : 0u;
+        uint32_t v = (own && t >= off) ? scratch[t - off] : 0u;
         __syncthreads();
-        scratch[t] += v;
+        if (own) scratch[t] += v;
         __syncthreads();
     }
-    uint32_t incl = scratch[t], excl = incl - s;
-    if (excl < k && incl >= k) {
+    uint32_t incl = own ? scratch[t] : 0u, excl = incl - s;
+    if (own && excl < k && incl >= k) {
         uint32_t run = excl;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -113,7 +114,8 @@ __device__ inline uint32_t key_bin(uint32_t key, int p) {
 // ------------------------------------------------------------------------------------------
 // TopK: sample threshold (one workgroup per row)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws) {
     __shared__ uint32_t keys[SMAX];
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
@@ -124,18 +126,21 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
     int S;
     if (d <= SMAX) {
         S = (int)d;
-        for (int i = threadIdx.x; i < S; i += 256) keys[i] = mag_key(r[i]);
+        for (int i = threadIdx.x; i < S; i += NT) keys[i] = mag_key(r[i]);
     } else {
         const int P = SMAX / 256;
         S = SMAX;
         // piece p = 256 contiguous elements at p (d - 256) / (P - 1); thread t reads element t of
         // 32 pieces per round trip (a lone row's sample is latency-bound: few trips)
+        // NT / 256 groups of threads take interleaved pieces
+        constexpr int GR = NT / 256, PU = 32 / GR;
+        const int e = threadIdx.x & 255, g0 = threadIdx.x >> 8;
         for (int p0 = 0; p0 < P; p0 += 32) {
-            float x[32];
+            float x[PU];
 #pragma unroll
-            for (int u = 0; u < 32; ++u) x[u] = r[((int64_t)(p0 + u) * (d - 256)) / (P - 1) + threadIdx.x];
+            for (int u = 0; u < PU; ++u) x[u] = r[((int64_t)(p0 + u * GR + g0) * (d - 256)) / (P - 1) + e];
 #pragma unroll
-            for (int u = 0; u < 32; ++u) keys[(p0 + u) * 256 + threadIdx.x] = mag_key(x[u]);
+            for (int u = 0; u < PU; ++u) keys[(p0 + u * GR + g0) * 256 + e] = mag_key(x[u]);
         }
     }
     // rank (from the top) of the sample element whose key is the threshold
@@ -151,9 +156,9 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
     auto rank_key = [&](uint32_t r) {
         uint32_t prefix = 0, krem = r;
         for (int p = 0; p < 3; ++p) {
-            for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
+            for (int i = threadIdx.x; i < HBINS; i += NT) h[i] = 0;
             __syncthreads();
-            for (int i = threadIdx.x; i < S; i += 256) {
+            for (int i = threadIdx.x; i < S; i += NT) {
                 uint32_t k = keys[i];
                 if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
             }
@@ -190,7 +195,8 @@ __global__ __launch_bounds__(256) void k_topk_sample(RowSrc rows, int64_t n, int
 // path.  Result as k_radix_select's last pass: thr = K-th key, krem = ties to admit, F_TIES when
 // the list has more keys equal to thr than that.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs ws) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_cand_select(int64_t n, int64_t K, SelWs ws) {
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
     for (int64_t row = blockIdx.x; row < n; row += gridDim.x) {
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
         while (true) {
             const int s1 = first ? sh : max(0, sh - 11);
             const uint32_t mask = first ? 0xFFFFFFFFu : ((1u << (sh - s1)) - 1u);
-            for (int i = threadIdx.x; i < HBINS; i += 256) h[i] = 0;
+            for (int i = threadIdx.x; i < HBINS; i += NT) h[i] = 0;
             __syncthreads();
             auto add = [&](float x) {
                 const uint32_t dk = mag_key(x) - T;
@@ -222,18 +228,18 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
             };
             // 8 float4 per thread in flight per round trip (the walk is latency-bound otherwise)
             uint32_t i = threadIdx.x;
-            for (; i + 7 * 256 < n4; i += 8 * 256) {
+            for (; i + 7 * NT < n4; i += 8 * NT) {
                 float4 q[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) q[u] = v4[i + u * 256];
+                for (int u = 0; u < 8; ++u) q[u] = v4[i + u * NT];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) { add(q[u].x); add(q[u].y); add(q[u].z); add(q[u].w); }
             }
-            for (; i < n4; i += 256) {
+            for (; i < n4; i += NT) {
                 const float4 q = v4[i];
                 add(q.x); add(q.y); add(q.z); add(q.w);
             }
-            for (uint32_t i = n4 * 4 + threadIdx.x; i < cnt; i += 256) add(vals[i]);
+            for (uint32_t i = n4 * 4 + threadIdx.x; i < cnt; i += NT) add(vals[i]);
             __syncthreads();
             uint32_t bin, above;
             hist_find(h, krem, bin, above, scratch);
@@ -258,19 +264,19 @@ __global__ __launch_bounds__(256) void k_cand_select(int64_t n, int64_t K, SelWs
             if (threadIdx.x == 0) scratch[0] = 0;
             __syncthreads();
             const uint32_t* idxs = ws.ent_idx + row * ws.cap;
-            for (uint32_t i = threadIdx.x; i < n4; i += 256) {
+            for (uint32_t i = threadIdx.x; i < n4; i += NT) {
                 const float4 q = v4[i];
                 const float qv[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (mag_key(qv[u]) == thr) tix[atomicAdd(&scratch[0], 1u)] = idxs[i * 4 + u];
             }
-            for (uint32_t i = n4 * 4 + threadIdx.x; i < cnt; i += 256) {
+            for (uint32_t i = n4 * 4 + threadIdx.x; i < cnt; i += NT) {
                 if (mag_key(vals[i]) == thr) tix[atomicAdd(&scratch[0], 1u)] = idxs[i];
             }
             __syncthreads();
             const uint32_t m = scratch[0];                              // == last
-            for (uint32_t a = threadIdx.x; a < m; a += 256) {
+            for (uint32_t a = threadIdx.x; a < m; a += NT) {
                 const uint32_t ia = tix[a];
                 uint32_t rank = 0;
                 for (uint32_t b = 0; b < m; ++b) rank += tix[b] < ia ? 1u : 0u;
@@ -1285,7 +1291,8 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         const int64_t bpr = (C + 3) / 4;
         if (!dense_k) {
             { ProfScope _ps("k_topk_sample", st);
-hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, K, ws); }
+if (n < 128) hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws);
+            else hipLaunchKernelGGL(k_topk_sample<256>, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, K, ws); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             { ProfScope _ps("k_topk_filter", st);
             // persistent grid: exactly the resident blocks (a second partial wave of blocks would
@@ -1294,7 +1301,9 @@ hipLaunchKernelGGL(k_topk_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, 
             else launch_filter<4>(rows, n, d, ws, st); }
             FLC_CHECK_LAUNCH("k_topk_filter");
             { ProfScope _ps("k_cand_select", st);
-            hipLaunchKernelGGL(k_cand_select, dim3(grid_stride_blocks(n, 8192)), dim3(256), 0, st, n, K, ws); }
+            // few rows (a lone compressVector): one 1024-thread workgroup per row walks the list 4x wider
+            if (n < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)n), dim3(1024), 0, st, n, K, ws);
+            else hipLaunchKernelGGL(k_cand_select<256>, dim3(grid_stride_blocks(n, 8192)), dim3(256), 0, st, n, K, ws); }
             FLC_CHECK_LAUNCH("k_cand_select");
         } else {
             FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
