@@ -1159,6 +1159,22 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
     }
 }
 
+// Single-row dense output (compressVector: out = zeros; out[admitted] = x, stored not added, so a
+// selected -0.0 stays -0.0 like torch's out[ind] = x[ind]): after a memset, the row's list
+// (entries [0, rowcnt), distinct indices) is scattered with the fold's admission rule — no per-chunk
+// tile walk for one row.
+__global__ __launch_bounds__(256) void k_assign_scatter(SelWs ws, float* __restrict__ out) {
+    const uint32_t cnt = ws.rowcnt[0], T = ws.thr[0], f = ws.flags[0];
+    const uint32_t mode = (f & F_EXACT) ? 2u : ((f & F_TIES) ? 1u : 0u);
+    const uint32_t cut = mode == 1u ? ws.tiecut[0] : 0xFFFFFFFFu;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < cnt; e += gridDim.x * 256u) {
+        const uint32_t ix = ws.ent_idx[e];
+        const float v = ws.ent_val[e];
+        const uint32_t key = mag_key(v);
+        if (mode == 2u || key > T || (key == T && ix <= cut)) out[ix] = v;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Host orchestration
 // ------------------------------------------------------------------------------------------
@@ -1331,6 +1347,13 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
+    if (assign && n == 1 && codec == FLC_TOPK) {
+        FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
+        const int sb = (int)std::max<int64_t>(1, std::min<int64_t>((sel_capacity(codec, d, K) + 255) / 256, 2048));
+        hipLaunchKernelGGL(k_assign_scatter, dim3(sb), dim3(256), 0, st, ws, out);
+        FLC_CHECK_LAUNCH("k_assign_scatter");
+        return FLC_OK;
+    }
     { ProfScope _ps("k_chunk_accum", st);
     // few chunks (short rows: C2's D = 1 M has 245): split each chunk's columns over 2 or 4 waves so
     // the latency-bound row walk runs on more of the chip (many chunks: one wave each, measured best)
