@@ -1313,7 +1313,8 @@ if (n < 128) hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(102
             { ProfScope _ps("k_topk_filter", st);
             // persistent grid: exactly the resident blocks (a second partial wave of blocks would
             // leave the chip half idle at the end); buffer loads need no 16 B row alignment
-            if (filter_group() == 2) launch_filter<2>(rows, n, d, ws, st);
+            // few rows: 2-chunk groups (twice the waves in flight for a lone row)
+            if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, d, ws, st);
             else launch_filter<4>(rows, n, d, ws, st); }
             FLC_CHECK_LAUNCH("k_topk_filter");
             { ProfScope _ps("k_cand_select", st);
