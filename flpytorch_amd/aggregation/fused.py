@@ -72,6 +72,8 @@ class UplinkReducer:
             base, ld, ptrs = None, 0, pt.data_ptr()
         if out is None:
             out = torch.empty(d, dtype=torch.float32, device=dev)
+        if n == 0:
+            return out.zero_()                                   # no clients (algorithms.py:2117-2118)
         t = self.comp.compressorType
         if t == CompressorType.RANDK_COMPRESSOR and randk_idx is not None:
             pat.d_randk_idx = randk_idx.data_ptr()
