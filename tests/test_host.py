@@ -187,3 +187,34 @@ def test_install_rebinds_every_shared_fold():
     for n in names:
         assert getattr(algos, n).serverGradient is orig[n]
     assert comps.initCompressor() == "ref"
+
+
+def test_install_mapping_matches_the_reference_classes(tmp_path):
+    """The class names install() rebinds are exactly the reference's algorithm classes that define a
+    serverGradient (read from fl_pytorch/utils/algorithms.py itself, imported in a subprocess with
+    the throwaway stubs of tests/golden/make_golden.py; skipped where the reference is absent)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    ref = "/root/reference/fl_pytorch"
+    if not os.path.isdir(ref):
+        pytest.skip("reference not mounted (GPU box / other hosts)")
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = f"""
+import json, sys, inspect
+sys.path.insert(0, {os.path.join(here, 'golden')!r})
+import make_golden
+make_golden._write_stubs({str(tmp_path)!r})
+sys.path.insert(0, {str(tmp_path)!r}); sys.path.insert(0, {ref + '/utils'!r}); sys.path.insert(0, {ref!r})
+from utils import algorithms
+names = sorted(n for n, c in inspect.getmembers(algorithms, inspect.isclass)
+               if c.__module__ == algorithms.__name__ and 'serverGradient' in c.__dict__)
+print(json.dumps(names))
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=str(tmp_path), env={**os.environ, "PYTHONDONTWRITEBYTECODE": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    ref_names = set(json.loads(r.stdout.strip().splitlines()[-1]))
+    ours = set(ag.PLAIN_FOLD) | set(ag.MASTER_FOLD) | set(ag.SHIFTED_FOLD) | {"FRECON"}
+    assert ours == ref_names, (sorted(ours ^ ref_names))
