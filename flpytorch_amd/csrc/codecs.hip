@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include "codec_ops.hpp"
+#include "wire_codes.hpp"
 
 namespace flc {
 
@@ -182,6 +183,67 @@ __global__ __launch_bounds__(256) void k_ew_dense(const float* __restrict__ x, i
     }
     for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
         out[j] = op.template apply<false>(x[j], j, op.col(j), smem_tab);
+}
+
+// ------------------------------------------------------------------------------------------
+// Encode straight to wire codes (flc_pack of the Q8 / Q16 / NAT16 formats): the dense value of
+// each element is formed exactly as k_ew_dense forms it and turned into its code in registers,
+// so the client's message costs one read of the row (plus the norm pass) and one write of codes.
+// ------------------------------------------------------------------------------------------
+template <class Op, bool VEC>
+__global__ __launch_bounds__(256) void k_ew_code(const float* __restrict__ x, int64_t d, Op op,
+                                                 const float* __restrict__ levels, int s, CodeArgs ca) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem_tab[];
+    if (Op::TABLE) op.set_table_ok(load_table(levels, s, smem_tab));
+    op.setup(0);
+    PayloadHeader* h = reinterpret_cast<PayloadHeader*>(ca.payload);
+    char* body = ca.payload + 16;
+    const float norm = ca.pn ? *ca.pn : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        h->fmt = (uint32_t)ca.fmt;
+        h->count = (uint32_t)d;
+        h->norm = norm;
+    }
+    const uint32_t sbit = ca.fmt == FMT_Q8 ? 0x80u : 0x8000u;
+    auto code = [&](float v) -> uint32_t {
+        return ca.fmt == FMT_NAT16 ? nat_code(v) : lev_code(v, ca.lv, ca.s, norm, sbit, &h->bad);
+    };
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t j0 = VEC ? (d / 4) * 4 : 0;
+    if (VEC) {
+        for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < d / 4; g += stride) {
+            uint32_t cs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cs[q] = op.col(g * 4 + q);
+            const float4 v = reinterpret_cast<const float4*>(x)[g];
+            const float4 e = op.row_fast() ? apply4<true>(op, v, g * 4, cs, smem_tab)
+                                           : apply4<false>(op, v, g * 4, cs, smem_tab);
+            const uint32_t c0 = code(e.x), c1 = code(e.y), c2 = code(e.z), c3 = code(e.w);
+            if (ca.fmt == FMT_Q8)
+                reinterpret_cast<uint32_t*>(body)[g] = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+            else
+                reinterpret_cast<uint2*>(body)[g] = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));
+        }
+    }
+    for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride) {
+        const uint32_t c = code(op.template apply<false>(x[j], j, op.col(j), smem_tab));
+        if (ca.fmt == FMT_Q8) reinterpret_cast<uint8_t*>(body)[j] = (uint8_t)c;
+        else reinterpret_cast<uint16_t*>(body)[j] = (uint16_t)c;
+    }
+}
+
+static int grid_cap(int64_t work, int64_t per_block, int64_t cap);
+
+template <class Op>
+static int launch_code(const float* x, int64_t d, Op op, const float* levels, int s, const CodeArgs& ca, hipStream_t st) {
+    if (d == 0) return FLC_OK;
+    const bool vec = ((uintptr_t)x & 15u) == 0;
+    const size_t lds = Op::TABLE ? (size_t)s * sizeof(float4) : 0;
+    const int grid = grid_cap(vec ? (d + 3) / 4 : d, 256, 4096);
+    if (vec) hipLaunchKernelGGL((k_ew_code<Op, true>), dim3(grid), dim3(256), lds, st, x, d, op, levels, s, ca);
+    else hipLaunchKernelGGL((k_ew_code<Op, false>), dim3(grid), dim3(256), lds, st, x, d, op, levels, s, ca);
+    FLC_CHECK_LAUNCH("k_ew_code");
+    return FLC_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -473,14 +535,15 @@ static int check_dither(const flc_codec_params* prm) {
 // One row encode (compressVector) or fused reduce over n rows (n >= 1).
 int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool vec, int64_t n, int64_t d,
            const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt,
-           void* ws, size_t ws_bytes, hipStream_t st, const ShiftArgs* sh) {
-    if (sh && (!dense || n != 1)) { set_error("ew_run: the shift form is one dense row"); return FLC_ERR_ARG; }
+           void* ws, size_t ws_bytes, hipStream_t st, const ShiftArgs* sh, const CodeArgs* ca) {
+    if ((sh || ca) && (!dense || n != 1)) { set_error("ew_run: the shift / code forms are one dense row"); return FLC_ERR_ARG; }
     const int codec = prm->codec;
     const bool compat = pat && pat->d_uniforms;
     const int64_t client0 = pat ? pat->client0 : 0;
     UniformSrc us{compat ? pat->d_uniforms : nullptr, (pat && pat->uniforms_ld) ? pat->uniforms_ld : d};
     auto go = [&](auto op, const float* levels, int s) -> int {
         if (sh) return launch_shift(src.base, d, op, levels, s, *sh, st);
+        if (ca) return launch_code(src.base, d, op, levels, s, *ca, st);
         if (dense) return launch_dense(src.base, d, op, levels, s, out, st);
         return launch_accum(src, vec, n, d, op, levels, s, w, wt, out, st);
     };

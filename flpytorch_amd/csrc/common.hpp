@@ -92,9 +92,17 @@ struct ShiftArgs {
     const float* hin;
     float* hout;
 };
+// flc_pack's fused encode -> code form (Q8 / Q16 / NAT16): payload header + body written directly
+struct CodeArgs {
+    int fmt;
+    char* payload;
+    const float* lv;     // the level table (dithering)
+    int s;
+    const float* pn;     // device norm the codes are relative to (dithering)
+};
 int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool vec, int64_t n, int64_t d,
            const float* pnorm_in, float* pnorm_out, bool dense, float* out, const float* w, float wt, void* ws,
-           size_t ws_bytes, hipStream_t st, const ShiftArgs* sh = nullptr);
+           size_t ws_bytes, hipStream_t st, const ShiftArgs* sh = nullptr, const CodeArgs* ca = nullptr);
 size_t shift_workspace(const flc_codec_params* prm, int64_t d);
 int encode_row(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
                const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes, hipStream_t st);

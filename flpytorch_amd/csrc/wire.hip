@@ -23,18 +23,9 @@
 // (levels[i] * sign) * norm reproduces the element's bits (guess rint(y s), then its neighbours,
 // then a binary search); elements no level reproduces are counted in the header's `bad` field
 // (never seen: the encode's outputs are of that form by construction; the tests assert 0).
-#include "common.hpp"
+#include "wire_codes.hpp"
 
 namespace flc {
-
-enum { FMT_F32 = 1, FMT_Q8 = 2, FMT_Q16 = 3, FMT_NAT16 = 4, FMT_SPARSE = 5, FMT_RANKK = 6 };
-struct PayloadHeader {
-    uint32_t fmt, count;
-    float norm;
-    uint32_t bad;          // elements whose code search failed (0 by construction)
-};
-
-__host__ __device__ inline int64_t a16(int64_t b) { return (b + 15) & ~int64_t(15); }
 
 int payload_format(const flc_codec_params* prm) {
     switch (prm->codec) {
@@ -56,60 +47,6 @@ int64_t payload_bytes(const flc_codec_params* prm, int64_t d) {
         case FMT_RANKK: return 16 + a16(4 * rk_payload_floats(prm, d));
         default: return 16 + a16(4 * d);
     }
-}
-
-// ---- level codes ------------------------------------------------------------------------------
-__device__ inline float lev_value(const float* lv, uint32_t idx, bool neg, float norm) {
-    return copysignf(lv[idx], neg ? -1.f : 1.f) * norm;
-}
-
-__device__ inline uint32_t lev_code(float v, const float* lv, int s, float norm, uint32_t sbit, uint32_t* bad) {
-    const uint32_t vb = __float_as_uint(v);
-    if (vb == 0u) return 0u;                                   // +0 (x == 0)
-    const bool neg = (vb >> 31) != 0u;
-    if (v != v) return sbit;                                   // NaN: -0 * non-finite norm
-    const float y = fabsf(v) / norm;
-    int g = (int)rintf(y * (float)s);
-    g = g < 0 ? 0 : (g > s ? s : g);
-    for (int dlt = 0; dlt < 3; ++dlt) {
-        const int c = dlt == 0 ? g : (dlt == 1 ? g - 1 : g + 1);
-        if (c >= 0 && c <= s && __float_as_uint(lev_value(lv, (uint32_t)c, neg, norm)) == vb)
-            return (neg ? sbit : 0u) | (uint32_t)c;
-    }
-    int lo = 0, hi = s;                                        // levels ascending: binary search on |v|
-    while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        const float m = fabsf(lev_value(lv, (uint32_t)mid, neg, norm));
-        if (__float_as_uint(lev_value(lv, (uint32_t)mid, neg, norm)) == vb) return (neg ? sbit : 0u) | (uint32_t)mid;
-        if (m < fabsf(v)) lo = mid + 1; else hi = mid - 1;
-    }
-    atomicAdd(bad, 1u);
-    return neg ? sbit : 0u;
-}
-
-__device__ inline float lev_decode(uint32_t code, const float* lv, float norm, uint32_t sbit) {
-    if (code == 0u) return 0.f;
-    return lev_value(lv, code & (sbit - 1u), (code & sbit) != 0u, norm);
-}
-
-// ---- natural codes ----------------------------------------------------------------------------
-__device__ inline uint32_t nat_code(float v) {
-    const uint32_t vb = __float_as_uint(v), sg = (vb >> 31) << 15;
-    if ((vb & 0x7FFFFFFFu) == 0u) return sg;
-    if (v != v) return 0x7FFFu;
-    if (isinf(v)) return sg | 0x7FFEu;
-    int e;
-    (void)frexpf(v, &e);                                       // |v| = 0.5 * 2^e (a power of two)
-    return sg | (uint32_t)(e - 1 + 16384);
-}
-
-__device__ inline float nat_decode(uint32_t c) {
-    const float sg = (c & 0x8000u) ? -1.f : 1.f;
-    const uint32_t m = c & 0x7FFFu;
-    if (m == 0u) return copysignf(0.f, sg);
-    if (m == 0x7FFFu) return __uint_as_float(0x7FC00000u);
-    if (m == 0x7FFEu) return copysignf(__builtin_inff(), sg);
-    return copysignf(ldexpf(1.f, (int)m - 16384), sg);
 }
 
 // ---- pack ---------------------------------------------------------------------------------------
@@ -141,6 +78,16 @@ __global__ __launch_bounds__(256) void k_pack_dense(const float* __restrict__ v,
         else if (fmt == FMT_Q8) reinterpret_cast<uint8_t*>(body)[j] = (uint8_t)lev_code(x, levels, s, norm, 0x80u, &h->bad);
         else if (fmt == FMT_Q16) reinterpret_cast<uint16_t*>(body)[j] = (uint16_t)lev_code(x, levels, s, norm, 0x8000u, &h->bad);
         else reinterpret_cast<uint16_t*>(body)[j] = (uint16_t)nat_code(x);
+    }
+}
+
+__global__ void k_pack_header(char* payload, uint32_t fmt, uint32_t count) {
+    if (threadIdx.x == 0) {
+        PayloadHeader* h = reinterpret_cast<PayloadHeader*>(payload);
+        h->fmt = fmt;
+        h->count = count;
+        h->norm = 0.f;
+        h->bad = 0u;
     }
 }
 
@@ -397,6 +344,22 @@ int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x
         return FLC_OK;
     }
     const bool dither = fmt == FMT_Q8 || fmt == FMT_Q16;
+    if (dither || fmt == FMT_NAT16) {
+        // one pass: the encode writes its codes straight into the payload (codecs.hip k_ew_code)
+        CodeArgs ca{fmt, payload, prm->d_levels, prm->s, dither ? w.pnorm : nullptr};
+        RowSrc src{x, d, nullptr};
+        return ew_run(prm, pat, src, ((uintptr_t)x & 15u) == 0, 1, d, nullptr, dither ? w.pnorm : nullptr,
+                      /*dense=*/true, nullptr, nullptr, 1.f, w.inner, w.inner_bytes, st, nullptr, &ca);
+    }
+    if (fmt == FMT_F32) {
+        // the dense encode written straight into the body, then the header
+        int rc = encode_row(prm, pat, x, d, nullptr, nullptr, reinterpret_cast<float*>(payload + 16), w.inner,
+                            w.inner_bytes, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_pack_header, dim3(1), dim3(64), 0, st, payload, (uint32_t)fmt, (uint32_t)d);
+        FLC_CHECK_LAUNCH("k_pack_header");
+        return FLC_OK;
+    }
     int rc = encode_row(prm, pat, x, d, nullptr, dither ? w.pnorm : nullptr, w.dense, w.inner, w.inner_bytes, st);
     if (rc) return rc;
     (void)natbug;
