@@ -105,8 +105,17 @@ def cpu_baseline(spec, d, budget_s=12.0, specs=None):
             break
     dt = time.perf_counter() - t0
     k = math.ceil(0.01 * d)
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
     return {"value": round(algorithmic_bytes(spec, rows, d, k, specs) / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
             "kind": "port",
+            # the host the baseline ran on
+            "host": {"cpu_model": cpu_model, "affinity_cpus": len(os.sched_getaffinity(0)),
+                     "torch_threads": torch.get_num_threads()},
             "sample": f"oracle/codecs.py {'/'.join(specs) if specs else spec}: pattern + encode + sequential fp32 reduce of {rows} rows x D={d} "
                       f"({dt:.1f} s, numpy single-threaded)"}
 
