@@ -18,6 +18,12 @@ FLC_OK, FLC_ERR_ARG, FLC_ERR_DTYPE, FLC_ERR_HIP, FLC_ERR_WORKSPACE, FLC_ERR_UNSU
 FLC_IDENT, FLC_LAZY, FLC_RANDK, FLC_NATURAL, FLC_STD_DITHERING, FLC_NAT_DITHERING, FLC_TOPK, FLC_RANK_K = range(1, 9)
 FLC_NORM_LINF, FLC_NORM_L1, FLC_NORM_L2 = 0, 1, 2
 FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
+# execution hints (flc_codec_params.flags): how, never what — every choice gives the same bits
+FLC_PATH_AUTO, FLC_PATH_SPARSE, FLC_PATH_DENSE = 0, 1, 2
+
+
+def FLC_ROW_GROUPS(g):
+    return (int(g) & 0xFF) << 8
 
 # every symbol include/flcodec.h declares (tests/test_abi.py checks the .so exports all of them)
 EXPORTS = [
@@ -41,7 +47,7 @@ class FlcCodecParams(ctypes.Structure):
         ("codec", ctypes.c_int32),
         ("s", ctypes.c_int32),
         ("norm", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
         ("k", ctypes.c_int64),
         ("lazy_p", ctypes.c_float),
         ("randk_scale", ctypes.c_float),

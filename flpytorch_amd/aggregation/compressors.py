@@ -136,6 +136,11 @@ class Compressor:
         self.compressorType = CompressorType.IDENTICAL
         self.resetStats()
         self.device_rng = None   # (seed, client) -> device counter-based patterns (opt-in)
+        # execution hints (flc_codec_params.flags); results are identical for every setting:
+        #   dither_path  None | "sparse" | "dense"  (QSGD p=2, device-RNG fused uplink)
+        #   row_groups   None | g                   (folds pipelined under the next group's pass)
+        self.dither_path = None
+        self.row_groups = None
 
     # -- constants -------------------------------------------------------------------------
     def fullName(self):
@@ -280,6 +285,12 @@ class Compressor:
             keep.append(self.levelsValues)
         if self.device_rng is not None:
             prm.seed = int(self.device_rng[0]) & 0xFFFFFFFFFFFFFFFF
+        flags = {None: _lib.FLC_PATH_AUTO, "sparse": _lib.FLC_PATH_SPARSE, "dense": _lib.FLC_PATH_DENSE}
+        if getattr(self, "dither_path", None) not in flags:
+            raise ValueError(f"dither_path must be None, 'sparse' or 'dense' (got {self.dither_path!r})")
+        prm.flags = flags[getattr(self, "dither_path", None)]
+        if getattr(self, "row_groups", None):
+            prm.flags |= _lib.FLC_ROW_GROUPS(self.row_groups)
         return prm, keep
 
     def _need_to_send(self, d):

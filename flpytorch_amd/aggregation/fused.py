@@ -14,7 +14,6 @@ Pattern sources
   * device  — counter-based draws keyed by (seed, client id, element) generated inside the
               kernels: no host work, no uniform bytes (the benchmark mode).
 """
-import contextlib
 import ctypes
 
 import torch
@@ -47,7 +46,16 @@ class UplinkReducer:
         """rows: [N, D] fp32 device tensor (row stride % 4 == 0 for the vector path) or a list of
         [D] device tensors.  Compat patterns: randk_idx [N, K] int64, uniforms [N, D] float64,
         lazy_u [N] float64 (device).  Without them (and with ``seed`` set) draws are on device.
-        ``divisor`` overrides the fp32 divisor sum(w) (e.g. 1.0 for a partial sum across GPUs)."""
+        ``divisor`` overrides the fp32 divisor sum(w) (e.g. 1.0 for a partial sum across GPUs).
+        ``stream``: every allocation, copy and the launch go to that stream (torch's stream
+        semantics: the caller orders it after the producers of ``rows`` and the patterns)."""
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor)
+        return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor)
+
+    def _run(self, rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor):
+        """The call on the current stream (allocations, uploads and the launch all on it)."""
         lib = _lib.load()
         dev = self.device
         prm, keep = self.params()
@@ -66,8 +74,7 @@ class UplinkReducer:
             keep.extend(rows)
             # pinned staging + async copy: no host wait on the work already queued on the stream
             host_pt = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).pin_memory()
-            with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-                pt = host_pt.to(dev, non_blocking=True)
+            pt = host_pt.to(dev, non_blocking=True)
             keep.append(pt)
             base, ld, ptrs = None, 0, pt.data_ptr()
         if out is None:
@@ -103,7 +110,7 @@ class UplinkReducer:
             total = float(divisor)
         ws_bytes = lib.flc_encode_reduce_workspace_size(ctypes.byref(prm), n, d)
         ws = _lib.WORKSPACE.get(dev, ws_bytes)
-        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _lib.stream_ptr(dev)
+        st = _lib.stream_ptr(dev)
         with torch.cuda.device(dev):
             rc = lib.flc_encode_reduce(ctypes.byref(prm), ctypes.byref(pat), ctypes.c_void_p(base), ld,
                                        ctypes.c_void_p(ptrs), n, d, ctypes.c_void_p(w_ptr), ctypes.c_float(total),

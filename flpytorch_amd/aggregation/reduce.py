@@ -31,14 +31,23 @@ def _weights_and_total(weights):
     return uniform, float(total)
 
 
+def _work_device(t):
+    """The GPU a tensor's fold runs on: its own device, or the current one for a host tensor."""
+    _lib.require_gpu()
+    return t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+
+
 def reduce_rows(x, rows, weights=None, relative=True, out=None):
     """out = (sum_i w_i * (x - rows_i)) / sum(w)   (relative=True, client models in)
        out = (sum_i w_i * rows_i) / sum(w)         (relative=False, client updates in)
 
-    ``rows`` is a list of fp32 device tensors shaped like ``x`` (or a 2-D [N, D] tensor).
+    ``rows`` is a list of fp32 device tensors shaped like ``x`` (or a 2-D [N, D] tensor), on
+    ``x``'s device; ``x`` must be a device tensor (the callers move host tensors first).
     """
     _lib.require_gpu()
     lib = _lib.load()
+    if not x.is_cuda:
+        raise ValueError("reduce_rows: x must be a device tensor (no CPU path)")
     dev = x.device
     n = rows.shape[0] if torch.is_tensor(rows) else len(rows)
     d = x.numel()
@@ -79,9 +88,8 @@ def reduce_client_models(clients_responses, clients, params_current, H):
     fl_dtype = H["fl_dtype"]
     if fl_dtype != torch.float32 or params_current.dtype != torch.float32:
         raise TypeError(f"flcodec reduces fp32 only (fl_dtype={fl_dtype})")
-    _lib.require_gpu()
     host = not params_current.is_cuda
-    dev = params_current.device if not host else torch.device("cuda", torch.cuda.current_device())
+    dev = _work_device(params_current)
     models, weights = [], []
     for i in range(clients):
         clients_responses.waitForItem()
@@ -166,12 +174,16 @@ def make_server_gradient_frecon(algorithms_module):
         u = reduce_client_models(clients_responses, clients, params_current, H)
         first = clients_responses.get(0)
         alpha = first["client_state"]['alpha']
+        # the q fold runs on the GPU the model fold used (a host params_current: the current
+        # device), its result returned to params_current's device
+        dev = _work_device(params_current)
         qs, weights = [], []
         for i in range(clients):
             cs = clients_responses.get(i)['client_state']
-            qs.append(cs['qi'].to(device=u.device, dtype=H["fl_dtype"]).reshape(-1))
+            qs.append(cs['qi'].to(device=dev, dtype=H["fl_dtype"]).reshape(-1))
             weights.append(cs['weight'])
-        q_avg = reduce_rows(u.reshape(-1), qs, weights, relative=False).reshape(u.shape)   # x: shape only
+        ud = u.reshape(-1).to(dev)                                                       # x: shape only
+        q_avg = reduce_rows(ud, qs, weights, relative=False).reshape(u.shape).to(params_current.device)
         for i in range(clients):
             del clients_responses.get(i)['client_state']['qi']
         h_prev = H['h_prev']

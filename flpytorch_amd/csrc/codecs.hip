@@ -435,7 +435,7 @@ static int launch_shift(const float* a, int64_t d, Op op, const float* levels, i
 // FLC_EW_TILE=<cols>x<pf> overrides (tuning runs only).
 static int ew_tile_variant() {
     static int v = [] {
-        const char* e = getenv("FLC_EW_TILE");
+        const char* e = tuning_env("FLC_EW_TILE");
         if (!e) return 0;
         if (!strcmp(e, "2x2")) return 1;
         if (!strcmp(e, "2x4")) return 2;

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/flcodec.h"
@@ -30,6 +31,18 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Layout / probe switches for A/B tuning runs.  Only a build with -DFLC_TUNING (tools/ab_build.sh
+// --tuning) reads them from the environment; the product library ignores the environment, so a
+// stray variable can never change a result.
+inline const char* tuning_env(const char* name) {
+#ifdef FLC_TUNING
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 // Kernel timing (flc_profile_enable): a scope records a hipEvent pair around one launch.
 extern bool g_prof_on;

@@ -558,15 +558,23 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
-// Filter variant (tuning runs: FLC_DS_GCAP=1024 doubles the per-item staging and list regions,
-// FLC_DS_GRID=res launches a resident-only grid instead of the oversubscribed one).
-struct DsVariant { int gcap; bool resident; int ap; int fgs; };
-static DsVariant ds_variant() {
-    DsVariant v{DS_GCAP, false, DS_AP, DS_FGS};
-    if (const char* e = getenv("FLC_DS_FGS")) v.fgs = atoi(e) == 4 ? 4 : DS_FGS;
-    if (const char* e = getenv("FLC_DS_AP")) v.ap = atoi(e);
-    if (const char* e = getenv("FLC_DS_GCAP")) v.gcap = atoi(e) == 1024 ? 1024 : DS_GCAP;
-    if (const char* e = getenv("FLC_DS_GRID")) v.resident = !strcmp(e, "res");
+// Filter variant.  The product build always takes the defaults; a -DFLC_TUNING build reads the
+// A/B switches once per process (FLC_DS_GCAP=1024 doubles the per-item staging and list regions,
+// FLC_DS_GRID=res launches a resident-only grid, FLC_DS_FGS=4 four-chunk items), so the
+// workspace query and the run always see the same variant.
+struct DsVariant { int gcap; bool resident; int ap; int fgs; int probe; int aprobe; };
+static const DsVariant& ds_variant() {
+    static const DsVariant v = [] {
+        DsVariant r{DS_GCAP, false, DS_AP, DS_FGS, 0, 0};
+        if (const char* e = tuning_env("FLC_DS_FGS")) r.fgs = atoi(e) == 4 ? 4 : DS_FGS;
+        if (const char* e = tuning_env("FLC_DS_AP")) r.ap = atoi(e);
+        if (const char* e = tuning_env("FLC_DS_GCAP")) r.gcap = atoi(e) == 1024 ? 1024 : DS_GCAP;
+        if (const char* e = tuning_env("FLC_DS_GRID")) r.resident = !strcmp(e, "res");
+        // probe modes measure parts of the filter / fold in isolation: their outputs are NOT valid
+        if (const char* e = tuning_env("FLC_DS_PROBE")) r.probe = atoi(e);
+        if (const char* e = tuning_env("FLC_DS_APROBE")) r.aprobe = atoi(e);
+        return r;
+    }();
     return v;
 }
 
@@ -593,23 +601,17 @@ static DsWs carve_ds(void* base, int64_t n, int64_t d, int gcap, int fgs, size_t
 }
 
 // Path choice: the sparse path pays when the expected candidate share (s / sqrt(D), the hi8
-// slack) keeps a filter item well inside its staging capacity.  FLC_DITHER_PATH=sparse|dense
-// forces one (tests, tuning).
-int ds_mode_env() {
-    const char* e = getenv("FLC_DITHER_PATH");
-    if (!e) return 0;
-    if (!strcmp(e, "sparse")) return 1;
-    if (!strcmp(e, "dense")) return 2;
-    return 0;
-}
+// slack) keeps a filter item well inside its staging capacity.  The caller's hint
+// (flc_codec_params.flags & FLC_PATH_MASK: FLC_PATH_SPARSE / FLC_PATH_DENSE) forces one; both
+// paths give the same bits.
 
 bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d) {
     if (prm->codec != FLC_STD_DITHERING || prm->norm != FLC_NORM_L2) return false;
     if (pat && pat->d_uniforms) return false;                    // compat draws: dense path
     if (prm->s < 1 || prm->s > DS_MAXS - 1 || !prm->d_levels || n < 1 || d < 1) return false;
     if (d >= (int64_t)0x7FFFFFFF) return false;
-    const int m = ds_mode_env();
-    if (m) return m == 1;
+    const int m = prm->flags & FLC_PATH_MASK;
+    if (m) return m == FLC_PATH_SPARSE;
     const double share = 1.1 * (double)prm->s / sqrt((double)d) + 0.003;
     return share * DS_FGS * CHUNK <= DS_GCAP / 1.4;
 }
@@ -617,7 +619,8 @@ bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n,
 size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     (void)prm;
     size_t b = 0;
-    carve_ds(nullptr, n, d, ds_variant().gcap, ds_variant().fgs, &b);
+    const DsVariant& v = ds_variant();
+    carve_ds(nullptr, n, d, v.gcap, v.fgs, &b);
     return b;
 }
 
@@ -632,25 +635,24 @@ std::mutex g_ds_mu;
 std::map<int, DsCtx> g_ds_ctx;
 }  // namespace
 
-static int ds_groups(int64_t n) {
-    if (const char* e = getenv("FLC_DS_GROUPS")) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), n));
-    return 1;   // measured: folds beside filters are starved (K = 2..8 no faster than 1)
+// Row groups of the fold pipeline: the caller's hint (FLC_ROW_GROUPS(g) in flags), else 1
+// (measured: folds beside an unrestricted filter are starved, K = 2..8 no faster than 1).
+static int ds_groups(const flc_codec_params* prm, int64_t n) {
+    const int g = (prm->flags >> 8) & 0xFF;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g ? g : 1, n));
 }
 
 int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d, const float* w,
            float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
-    const DsVariant v = ds_variant();
+    const DsVariant& v = ds_variant();
     size_t need = 0;
     carve_ds(nullptr, n, d, v.gcap, v.fgs, &need);
     if (ws_bytes < need) { set_error("dithering (sparse): workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
     DsWs ws = carve_ds(wsp, n, d, v.gcap, v.fgs, nullptr);
     const int64_t client0 = pat ? pat->client0 : 0;
     const int64_t H = nhalves(d);
-    const char* pe = getenv("FLC_DS_PROBE");
-    const int probe = pe ? atoi(pe) : 0;
-    const char* ape = getenv("FLC_DS_APROBE");
-    const int aprobe = ape ? atoi(ape) : 0;
-    const int K = ds_groups(n);
+    const int probe = v.probe, aprobe = v.aprobe;
+    const int K = ds_groups(prm, n);
 
     auto filter = [&](int64_t r0, int64_t rn) -> int {
         auto launch = [&](auto kern) {

@@ -105,14 +105,13 @@ extern "C" int flc_mt_rand(uint32_t* h_key, int32_t* h_pos, int64_t n, double* h
         return FLC_ERR_ARG;
     }
     Mt mt{h_key, h_pos, 0};
-    int64_t i = 0;
-    // a pair straddling the end of the 624-word block: the scalar path
-    while (i < n && (*h_pos & 1) && *h_pos < 624) h_out[i++] = mt.next_double();
-    if (i == n) return FLC_OK;
-    // 1) sequential: the raw (untempered) words of the remaining draws, block by block, parked in
-    //    the output array itself (a pair of words occupies exactly the 8 bytes of its double);
-    uint32_t* raw = reinterpret_cast<uint32_t*>(h_out + i);
-    const int64_t m_total = n - i;
+    if (n == 0) return FLC_OK;
+    // 1) sequential: the raw (untempered) words of the draws, block by block, parked in the
+    //    output array itself (a pair of words occupies exactly the 8 bytes of its double).  The
+    //    words are copied in stream order before each twist, so a pair that straddles the end of
+    //    a 624-word block (any odd start position) needs no special case.
+    uint32_t* raw = reinterpret_cast<uint32_t*>(h_out);
+    const int64_t m_total = n;
     int64_t w = 0;
     while (w < 2 * m_total) {
         if (*h_pos >= 624) mt.twist();

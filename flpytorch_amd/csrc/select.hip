@@ -1056,6 +1056,67 @@ __device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64
 }
 
 
+// Sign of zero.  The reference adds every client's DENSE row, so a column a row did not keep
+// receives the term w_i * (+0) (-0 when w_i's sign bit is set).  The fold skips those terms and
+// starts its tile at -0 (the additive identity), which gives the same bits for every nonzero
+// result.  A sum is -0 only if every term was -0: the tile ends at -0 exactly when every KEPT
+// term was -0 (or none was kept), and the reference's sum is then -0 iff, in addition, every row
+// that did not keep the column has a negative-signed weight.  Those columns are resolved here:
+// for each row with a positive-signed weight (stopping once no candidate is left) the -0
+// columns it does not keep turn +0.  Untouched columns die at the first such row, so this costs
+// one extra list walk for chunks that have them and nothing for the others.
+template <int TS>
+__device__ void resolve_neg_zero(float* tl, uint32_t* rm, const SelWs& ws, int64_t c, int64_t n, uint32_t cbase,
+                                 int64_t len, const float* w, int lane) {
+    constexpr int NW = TS / 32;                        // mask words (32 columns each)
+    constexpr int WL = (NW + 63) / 64;                 // mask words per lane (word k = lane + 64 j)
+    bool any = false;
+    for (int k = 0; k < TS / 64; ++k) {
+        const int64_t i = (int64_t)k * 64 + lane;
+        const uint64_t b = __ballot(i < len && __float_as_uint(tl[i]) == 0x80000000u);
+        if (lane == 0) { rm[2 * k] = (uint32_t)b; rm[2 * k + 1] = (uint32_t)(b >> 32); }
+        any |= b != 0ull;
+    }
+    if (!any) return;
+    uint32_t z0[WL], zc[WL];
+#pragma unroll
+    for (int j = 0; j < WL; ++j) {
+        const int k = lane + 64 * j;
+        z0[j] = k < NW ? rm[k] : 0u;
+        zc[j] = z0[j];
+    }
+    for (int64_t r = 0; r < n; ++r) {
+        if (w && (__float_as_uint(w[r]) >> 31)) continue;      // its skipped term is -0: no constraint
+#pragma unroll
+        for (int j = 0; j < WL; ++j) if (lane + 64 * j < NW) rm[lane + 64 * j] = 0u;
+        const RowMeta m = load_meta(ws, c, n, r, w);
+        const uint32_t mode = m.mode, T = m.thr, cut = m.cut;
+        for (uint32_t e = (uint32_t)lane; e < m.te.y; e += 64) {
+            const uint32_t ix = ws.ent_idx[r * ws.cap + m.te.x + e];
+            const uint32_t key = mag_key(ws.ent_val[r * ws.cap + m.te.x + e]);
+            const uint32_t loc = ix - cbase;
+            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut)))
+                atomicOr(&rm[loc >> 5], 1u << (loc & 31));
+        }
+        bool left = false;
+#pragma unroll
+        for (int j = 0; j < WL; ++j) {
+            if (lane + 64 * j < NW) zc[j] &= rm[lane + 64 * j];
+            left |= zc[j] != 0u;
+        }
+        if (__ballot(left) == 0ull) break;
+    }
+#pragma unroll
+    for (int j = 0; j < WL; ++j) {
+        uint32_t dead = z0[j] & ~zc[j];
+        while (dead) {
+            const int b = __builtin_ctz(dead);
+            dead &= dead - 1u;
+            tl[(lane + 64 * j) * 32 + b] = 0.f;
+        }
+    }
+}
+
 // TS < CHUNK: a wave owns TS columns of a chunk (CHUNK / TS waves read the same lists and each
 // folds its part): a smaller LDS tile per wave, so more waves per CU hide the list latency.
 template <bool ASSIGN, int TS = CHUNK>
@@ -1063,6 +1124,7 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
                                                      float wt, float* __restrict__ out) {
     constexpr int PARTS = CHUNK / TS;
     __shared__ __attribute__((aligned(16))) float tile[4][TS];
+    __shared__ uint32_t zmask[4][TS / 32];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t C = nchunks(d);
@@ -1070,7 +1132,8 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
     const int64_t nb = (n + 63) / 64;                  // row batches
     for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < C * PARTS; t += (int64_t)gridDim.x * 4) {
         const int64_t c = t / PARTS;
-        for (int i = lane; i < TS; i += 64) tl[i] = 0.f;
+        // ASSIGN (compressVector: out = zeros, out[kept] = x) stores into +0; the fold adds into -0
+        for (int i = lane; i < TS; i += 64) tl[i] = ASSIGN ? 0.f : -0.f;
         const uint32_t cbase = (uint32_t)(c * CHUNK + (t % PARTS) * TS);
         RowMeta cur = load_meta(ws, c, n, lane, w), nxt;
         // ring of AP rows' entries (the first 128 of each list; range-checked buffer loads, lanes
@@ -1155,6 +1218,7 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
             cur = nxt;
         }
         const int64_t len = min((int64_t)TS, d - (int64_t)cbase);
+        if (!ASSIGN) resolve_neg_zero<TS>(tl, zmask[wv], ws, c, n, cbase, len, w, lane);
         for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
     }
 }
@@ -1231,7 +1295,7 @@ static int grid_stride_blocks(int64_t items, int64_t cap = 4096) {
 // Runs the TopK / RandK pipeline for n rows and writes out (ASSIGN: n == 1 dense encode).
 static int accum_parts() {
     static const int p = [] {
-        const char* e = getenv("FLC_ACCUM_PARTS");   // tuning runs only (0 / unset: by chunk count)
+        const char* e = tuning_env("FLC_ACCUM_PARTS");   // tuning runs only (0 / unset: by chunk count)
         const int v = e ? atoi(e) : 0;
         return (v == 1 || v == 2 || v == 4) ? v : 0;
     }();
@@ -1240,7 +1304,7 @@ static int accum_parts() {
 
 static int filter_group() {
     static const int g = [] {
-        const char* e = getenv("FLC_FILTER_GS");     // tuning runs only
+        const char* e = tuning_env("FLC_FILTER_GS");     // tuning runs only
         return (e && atoi(e) == 2) ? 2 : 4;
     }();
     return g;
@@ -1272,7 +1336,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         const int64_t ldi = (pat && pat->idx_ld) ? pat->idx_ld : K;
         flc_pattern p = pat ? *pat : flc_pattern{};
         dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>((K + 255) / 256, 64)), (unsigned)n);
-        if (!getenv("FLC_RANDK_GLOBAL")) {
+        if (!tuning_env("FLC_RANDK_GLOBAL")) {
             const int64_t spc = rk_spc(C), sb = (C + spc - 1) / spc;
             { ProfScope _ps("k_randk_coarse", st);
             if (spc == 1)

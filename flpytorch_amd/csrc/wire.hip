@@ -338,9 +338,9 @@ int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x
         FLC_CHECK_HIP(hipMemsetAsync(payload + pb - 16, 0, 16, st));
     }
     if (d == 0) {
-        PayloadHeader h{(uint32_t)fmt, 0u, 0.f, 0u};
-        FLC_CHECK_HIP(hipMemcpyAsync(payload, &h, sizeof(h), hipMemcpyHostToDevice, st));
-        FLC_CHECK_HIP(hipStreamSynchronize(st));     // h lives on this stack frame
+        // header {fmt, 0, 0, 0} written by a kernel: no host staging, no synchronisation
+        hipLaunchKernelGGL(k_pack_header, dim3(1), dim3(64), 0, st, payload, (uint32_t)fmt, 0u);
+        FLC_CHECK_LAUNCH("k_pack_header");
         return FLC_OK;
     }
     const bool dither = fmt == FMT_Q8 || fmt == FMT_Q16;

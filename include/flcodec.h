@@ -56,12 +56,24 @@ typedef enum {
 #define FLC_NORM_L2 2
 #define FLC_NORM_LINF 0
 
+/* Execution hints (flc_codec_params.flags).  They choose HOW a result is computed, never WHAT:
+ * every combination gives the same bits.  0 = the library's choice.
+ *   bits 0-1  dithering p = 2 in device-RNG mode: FLC_PATH_SPARSE (one-read candidate filter +
+ *             exact fold) or FLC_PATH_DENSE (norm pass, then encode pass)
+ *   bits 8-15 fused encode+reduce: number of row groups whose folds are pipelined under the
+ *             next group's streaming pass (FLC_ROW_GROUPS(g), g in 1..255) */
+#define FLC_PATH_AUTO 0
+#define FLC_PATH_SPARSE 1
+#define FLC_PATH_DENSE 2
+#define FLC_PATH_MASK 3
+#define FLC_ROW_GROUPS(g) (((g) & 0xFF) << 8)
+
 /* Codec configuration — the constants Compressor.make* sets (compressors.py:64-178). */
 typedef struct {
     int32_t codec;          /* flc_codec */
     int32_t s;              /* dithering: number of level intervals (levels has s+1 entries) */
     int32_t norm;           /* dithering: FLC_NORM_* */
-    int32_t reserved;
+    int32_t flags;          /* execution hints (FLC_PATH_*, FLC_ROW_GROUPS), 0 = library default */
     int64_t k;              /* randk / topk: K */
     float lazy_p;           /* lazy: P */
     float randk_scale;      /* randk: (float)(D / K) as the reference's fp32 scalar multiply */

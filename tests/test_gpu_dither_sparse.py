@@ -5,7 +5,8 @@ keeps the elements that could be nonzero (against a sampled lower bound of the n
 owners encode them exactly.  Bar: BIT-EXACT (uint32 compare) against the oracle — the reference's
 op order (oracle/codecs.py, compressors.py:270-299) with the device draws restated in numpy
 (oracle/devrng.py) — including the sign of zero, and bit-identical to the dense two-pass path at
-C4 scale.  FLC_DITHER_PATH=sparse|dense forces a path (the automatic choice keeps small D dense).
+C4 scale.  Compressor.dither_path = "sparse" | "dense" (the flc_codec_params.flags hint) forces a
+path; the automatic choice keeps small D dense.
 """
 import zlib
 
@@ -55,6 +56,13 @@ def oracle_uplink(spec, rows, client0, weights=None, seed=SEED):
     return oc.reduce_plain(enc, weights), np.array(norms, dtype=np.float32)
 
 
+def sparse(ag, spec, d):
+    """A compressor whose fused uplink is forced onto the sparse path (flags hint)."""
+    c = ag.initCompressor(spec, d)
+    c.dither_path = "sparse"
+    return c
+
+
 def make_rows(kind, n, d, g):
     if kind == "normal":
         return g.standard_normal((n, d)).astype(np.float32)
@@ -84,11 +92,10 @@ def make_rows(kind, n, d, g):
 @pytest.mark.parametrize("kind", ["normal", "heavy", "sparse", "negative", "clustered", "ones", "tiny"])
 @pytest.mark.parametrize("spec", ["qsgd:4", "qsgd:127"])
 def test_sparse_dither_vs_oracle(ag, monkeypatch, kind, spec):
-    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
     n, d, client0 = 5, 300_001, 11
     rows = make_rows(kind, n, d, np.random.default_rng(zlib.crc32(f"{kind}{spec}".encode())))
     want, wn = oracle_uplink(spec, rows, client0)
-    red = ag.UplinkReducer(ag.initCompressor(spec, d), seed=SEED)
+    red = ag.UplinkReducer(sparse(ag, spec, d), seed=SEED)
     pn = torch.empty(n, device="cuda")
     got = red(torch.from_numpy(rows).cuda(), client0=client0, pnorms_out=pn)
     assert_bitexact(pn, wn)
@@ -98,11 +105,10 @@ def test_sparse_dither_vs_oracle(ag, monkeypatch, kind, spec):
 @pytest.mark.parametrize("d", [1, 3, 4096, 4097, 8192 * 3 + 5, 16384, 16385, 100_000])
 def test_sparse_dither_shapes(ag, monkeypatch, d):
     """Chunk / item / sample boundaries, tiny rows (whole-row sample)."""
-    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
     n, client0 = 3, 0
     rows = np.random.default_rng(d).standard_normal((n, d)).astype(np.float32)
     want, _ = oracle_uplink("qsgd:16", rows, client0)
-    red = ag.UplinkReducer(ag.initCompressor("qsgd:16", d), seed=SEED)
+    red = ag.UplinkReducer(sparse(ag, "qsgd:16", d), seed=SEED)
     assert_bitexact(red(torch.from_numpy(rows).cuda(), client0=client0), want)
     # the pointer-array entry point reads the same rows
     rt = torch.from_numpy(rows).cuda()
@@ -113,7 +119,6 @@ def test_sparse_dither_shapes(ag, monkeypatch, d):
 def test_sparse_dither_weights_nonfinite(ag, monkeypatch, bad):
     """Weights (some negative, one zero) flip zero signs; a row with a NaN (norm NaN: every
     output NaN, as in the reference) or an inf element (norm inf) is folded dense."""
-    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
     n, d, client0 = 6, 120_000, 5
     g = np.random.default_rng(3)
     rows = make_rows("negative", n, d, g)
@@ -124,7 +129,7 @@ def test_sparse_dither_weights_nonfinite(ag, monkeypatch, bad):
         rows[5, 31] = np.inf
     w = [0.5, -2.0, 1.0, 0.0, 3.0, 1.25]
     want, _ = oracle_uplink("qsgd:8", rows, client0, weights=w)
-    red = ag.UplinkReducer(ag.initCompressor("qsgd:8", d), seed=SEED)
+    red = ag.UplinkReducer(sparse(ag, "qsgd:8", d), seed=SEED)
     assert_bitexact(red(torch.from_numpy(rows).cuda(), client0=client0, weights=w), want)
 
 
@@ -133,8 +138,6 @@ def test_sparse_dither_weights_nonfinite(ag, monkeypatch, bad):
 def test_sparse_dither_row_groups(ag, monkeypatch, groups, weighted):
     """The row-group pipeline (filter of group g+1 beside the fold of group g on a side stream; the
     folds continue each other's sums) gives the same bits as the sequential fold."""
-    monkeypatch.setenv("FLC_DITHER_PATH", "sparse")
-    monkeypatch.setenv("FLC_DS_GROUPS", str(groups))
     n, d, client0 = 7, 150_001, 3
     g = np.random.default_rng(groups)
     rows = make_rows("normal", n, d, g)
@@ -142,7 +145,9 @@ def test_sparse_dither_row_groups(ag, monkeypatch, groups, weighted):
     rows[5] = make_rows("clustered", 1, d, g)[0]          # a dense-folded row inside a group
     w = [1.0, -0.5, 2.0, 1.5, 0.25, 1.0, 3.0] if weighted else None
     want, wn = oracle_uplink("qsgd:16", rows, client0, weights=w)
-    red = ag.UplinkReducer(ag.initCompressor("qsgd:16", d), seed=SEED)
+    comp = sparse(ag, "qsgd:16", d)
+    comp.row_groups = groups
+    red = ag.UplinkReducer(comp, seed=SEED)
     pn = torch.empty(n, device="cuda")
     got = red(torch.from_numpy(rows).cuda(), client0=client0, weights=w, pnorms_out=pn)
     torch.cuda.synchronize()
@@ -155,10 +160,11 @@ def test_sparse_equals_dense_c4_scale(ag, monkeypatch):
     the same bits, and the same norms (the oracle would take minutes at this size)."""
     n, d = 6, 25_000_000
     x = torch.empty((n, d), device="cuda").normal_(generator=torch.Generator("cuda").manual_seed(4))
-    red = ag.UplinkReducer(ag.initCompressor("qsgd:127", d), seed=SEED)
+    comp = ag.initCompressor("qsgd:127", d)
+    red = ag.UplinkReducer(comp, seed=SEED)
     outs, norms = {}, {}
     for path in ("sparse", "dense"):
-        monkeypatch.setenv("FLC_DITHER_PATH", path)
+        comp.dither_path = path
         pn = torch.empty(n, device="cuda")
         outs[path] = red(x, client0=100, pnorms_out=pn).cpu().numpy()
         norms[path] = pn.cpu().numpy()
@@ -170,9 +176,9 @@ def test_sparse_equals_dense_c4_scale(ag, monkeypatch):
 
 def test_auto_path_choice(ag, monkeypatch):
     """Without the override, C4's shape takes the sparse path and short rows the dense one
-    (checked through the library's launch profiler)."""
+    (checked through the library's launch profiler); the environment never changes the path."""
     from flpytorch_amd import _lib
-    monkeypatch.delenv("FLC_DITHER_PATH", raising=False)
+    monkeypatch.setenv("FLC_DITHER_PATH", "dense")       # read only by -DFLC_TUNING builds
     for d, want, other in ((25_000_000, "k_ds_filter", "k_ew_accum_vec"), (200_000, "k_ew_accum_vec", "k_ds_filter")):
         x = torch.randn((2, d), device="cuda")
         red = ag.UplinkReducer(ag.initCompressor("qsgd:127", d), seed=SEED)

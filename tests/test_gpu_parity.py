@@ -452,3 +452,84 @@ def test_gradskip_and_frecon_server_gradients(ag):
     assert_bitexact(out, want.numpy())
     assert all("qi" not in it["client_state"] for it in items)
     assert H["alpha_update"] == 0.25 * (n / 20)
+
+
+def test_frecon_with_host_params(ag):
+    """FRECON's serverGradient with a HOST params_current (the simulator's CPU model, device rows):
+    both folds run on the GPU and the result lands on the host, equal to the device-params run."""
+    import types
+
+    class Buf:
+        def __init__(self, items):
+            self.items = items
+
+        def waitForItem(self):
+            pass
+
+        def get(self, i):
+            return self.items[i]
+    g = np.random.default_rng(7)
+    n, d = 4, 2049
+    x = g.standard_normal(d).astype(np.float32)
+    models = [g.standard_normal(d).astype(np.float32) for _ in range(n)]
+    qs = [g.standard_normal(d).astype(np.float32) for _ in range(n)]
+    gprev = g.standard_normal(d).astype(np.float32)
+    hprev = g.standard_normal(d).astype(np.float32)
+    am = types.SimpleNamespace(has_experiment_option=lambda H, k: k == "lambda_",
+                               get_experiment_option_f=lambda H, k: 0.3)
+    outs = []
+    for on_host in (False, True):
+        dev = "cpu" if on_host else "cuda"
+        items = [{"model": torch.from_numpy(m.copy()), "client_state": {"weight": 1.0, "alpha": 0.5,
+                                                                        "qi": torch.from_numpy(qs[i].copy()).cuda()}}
+                 for i, m in enumerate(models)]
+        H = {"fl_dtype": torch.float32, "h_prev": torch.from_numpy(hprev).to(dev),
+             "g_server_prev": torch.from_numpy(gprev).to(dev), "total_clients": 8}
+        out = ag.make_server_gradient_frecon(am)(Buf(items), n, None, torch.from_numpy(x).to(dev), H)
+        assert out.device.type == dev
+        outs.append(out.cpu().numpy())
+    assert_bitexact(outs[1], outs[0])
+
+
+@pytest.mark.parametrize("spec", ["topk:3%", "randk:3%"])
+@pytest.mark.parametrize("n", [1, 2, 5])
+@pytest.mark.parametrize("weights", ["ones", "mixed", "negative"])
+def test_signed_zero_in_sparse_fold(ag, spec, n, weights):
+    """Columns whose every kept value is -0 (the chunk-owner fold gave +0).  The
+    reference adds the dense rows, so the result is -0 iff EVERY term is -0: kept -0 values, and
+    w_i * (+0) for the rows that did not keep the column (-0 only for negative-signed weights).
+    Bit-exact against the oracle's sequential fold, untouched columns included."""
+    d = 3 * 4096 + 77
+    g = np.random.default_rng(n * 7 + len(weights))
+    rows = np.zeros((n, d), dtype=np.float32)
+    k = math.ceil(0.03 * d)
+    idx = []
+    for i in range(n):
+        # 40 large values per row, the rest +0, and -0 at the lowest indices: TopK keeps the 40
+        # large ones and fills K from the lowest-index zeros (ties by lowest index) -> the -0s
+        big = g.choice(np.arange(200, d), 40, replace=False)
+        rows[i, big] = g.standard_normal(40).astype(np.float32) * 10
+        rows[i, :150] = -0.0
+        rows[i, 150:160] = 0.0
+        if i == n - 1 and n > 1:
+            rows[i, 100:150] = 0.0                           # the last client: +0 at some of them
+        # RandK (compat indices): every client keeps 0..199 plus its own random others
+        rest = g.choice(np.arange(200, d), k - 200, replace=False)
+        idx.append(np.concatenate([np.arange(200), rest]).astype(np.int64))
+    w = {"ones": None, "mixed": [1.0, -2.0, 0.5, -0.0, 3.0][:n], "negative": [-1.0, -0.5, -2.0, -1.5, -3.0][:n]}[weights]
+    enc = []
+    for i in range(n):
+        o = oc.OracleCompressor(spec, d)
+        o.S = idx[i]
+        enc.append(o.compress(rows[i]))
+    want = oc.reduce_plain(enc, w)
+    kw = {"randk_idx": torch.from_numpy(np.stack(idx)).cuda()} if spec.startswith("randk") else {}
+    red = ag.UplinkReducer(ag.initCompressor(spec, d))
+    got = red(torch.from_numpy(rows).cuda(), weights=w, **kw)
+    assert (want[:100] == 0).all() and (want[200:] == 0).any()      # kept -0 columns and untouched ones
+    if weights == "ones":
+        assert np.signbit(want[:100]).all()                           # ... that the reference returns as -0
+    assert_bitexact(got, want)
+    # the pointer-array entry point and the wire path (sparse payloads) give the same bits
+    rt = torch.from_numpy(rows).cuda()
+    assert_bitexact(red([rt[i].clone() for i in range(n)], weights=w, **kw), want)

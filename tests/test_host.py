@@ -46,6 +46,27 @@ def test_stream_matches_numpy_and_oracle(seed):
     np.testing.assert_array_equal(rs_ag.randint(0, 1000, 50), rs_np.randint(0, 1000, 50))
 
 
+@pytest.mark.parametrize("odd_words", [1, 3, 623])
+def test_stream_rand_from_an_odd_position(odd_words):
+    """rand(D) after an odd number of 32-bit draws (each client's randint(2**31),
+    algorithms.py:2055, flips the parity): bit-exact, and on the block-copy path (fast)."""
+    import time
+    rs_np, rs_ag = np.random.RandomState(77), np.random.RandomState(77)
+    for _ in range(odd_words):
+        assert int(ag.stream_randint31(rs_ag)[0]) == rs_np.randint(2 ** 31)
+    assert rs_ag.get_state()[2] % 2 == 1
+    for n in (1, 2, 623, 624, 625, 1249):
+        np.testing.assert_array_equal(ag.stream_rand(rs_ag, n), rs_np.rand(n))
+    assert rs_ag.get_state()[2] % 2 == 1          # rand draws words in pairs: still odd
+    n = 4_000_000
+    t0 = time.perf_counter()
+    got = ag.stream_rand(rs_ag, n)
+    dt = time.perf_counter() - t0
+    np.testing.assert_array_equal(got, rs_np.rand(n))
+    assert rs_ag.get_state()[2] == rs_np.get_state()[2]
+    assert dt < 0.5, f"rand({n}) from an odd position took {dt:.2f} s (scalar path?)"
+
+
 def test_stream_rejects_other_generators():
     with pytest.raises((TypeError, AttributeError)):
         ag.stream_choice(np.random.default_rng(0), 10, 3)
