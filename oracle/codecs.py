@@ -171,17 +171,20 @@ class OracleCompressor:
                 need = 9.0 / 32.0 * d
             elif t in (STD_DITHERING, NAT_DITHERING):
                 pn = self.norm(x) if pnorm is None else _F32(pnorm)
-                out = np.zeros_like(x)
                 sign = np.sign(x)
                 y = np.abs(x) / pn
                 lv = self.levels
                 u = self.testp
-                for s in range(len(lv) - 1):
-                    c12 = (y >= lv[s]) & (y <= lv[s + 1])
-                    p = (y - lv[s + 1]) / (lv[s] - lv[s + 1])
-                    c3 = u < p.astype(np.float64)
-                    out[c12 & c3] = lv[s]
-                    out[c12 & ~c3] = lv[s + 1]
+                if d <= LOOP_MAX_D:
+                    out = np.zeros_like(x)
+                    for s in range(len(lv) - 1):
+                        c12 = (y >= lv[s]) & (y <= lv[s + 1])
+                        p = (y - lv[s + 1]) / (lv[s] - lv[s + 1])
+                        c3 = u < p.astype(np.float64)
+                        out[c12 & c3] = lv[s]
+                        out[c12 & ~c3] = lv[s + 1]
+                else:
+                    out = dither_levels(y, u, lv)
                 out[x == 0.0] = 0.0
                 if t == STD_DITHERING:
                     out = out * sign * pn
@@ -205,6 +208,30 @@ class OracleCompressor:
         self.really_need_to_send_components += need
         self.total_input_components += d
         return out
+
+
+# Above this D the dithering level loop (O(s D) numpy passes, compressors.py:284-291) is replaced by
+# dither_levels, its closed form; tests/test_oracle_golden.py pins the two equal.
+LOOP_MAX_D = 1 << 20
+
+
+def dither_levels(y, u, lv):
+    """Closed form of the reference's level loop (compressors.py:284-291) in one pass.
+
+    The loop visits the intervals s = 0..S-1 in order and assigns to every element with
+    lv[s] <= y <= lv[s+1]; an element on a level boundary lies in two intervals and the LATER one
+    wins, so the effective interval is the largest s with lv[s] <= y, clipped to S-1 when
+    y == lv[S]; y above lv[S] (or NaN) lies in none and stays 0.  Inside it the same fp32
+    arithmetic: p = (y - lv[s+1]) / (lv[s] - lv[s+1]), lv[s] if u < p (float64 compare) else lv[s+1]."""
+    S = len(lv) - 1
+    s = np.searchsorted(lv, y, side="right").astype(np.int64) - 1
+    inside = (s >= 0) & ((s < S) | (y == lv[S]))
+    s = np.clip(s, 0, S - 1)
+    lo, hi = lv[s], lv[s + 1]
+    p = (y - hi) / (lo - hi)
+    out = np.where(u < p.astype(np.float64), lo, hi).astype(_F32)
+    out[~inside] = 0.0
+    return out
 
 
 def topk_keys(x):

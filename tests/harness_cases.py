@@ -1,0 +1,36 @@
+"""Shared setup of the round-harness tests: the reference runs captured by
+tests/golden/make_golden_harness.py (harness.json / harness.npz) replayed through
+flpytorch_amd.harness.Simulation."""
+import numpy as np
+
+from tests.golden_io import load
+
+META, DATA = load("harness")
+RUN_NAMES = sorted(META)
+
+
+def simulation(name, device, **kw):
+    from flpytorch_amd import harness
+    m = META[name]
+    model = harness.DenseModel(DATA["data_A"], DATA["data_B"], m["samples_per_client"])
+    assert model.D == m["D"]
+    return harness.Simulation(m["algorithm"], m["client_compressor"], model, DATA[f"{name}_x0"], m["num_clients"],
+                              m["clients_per_round"], m["rounds"], m["local_lr"], m["global_lr"],
+                              local_iters=m["local_iters"], runtime_seed=m["manual_runtime_seed"], device=device, **kw)
+
+
+def check_history(name, H, rel=1e-6):
+    """Per round: the sampled clients in Buffer order, each client's f values and wire counts, and the
+    history scalars of serverGlobalStateUpdate (algorithms.py:2218-2223) within `rel` of the
+    reference's."""
+    want = META[name]["history"]
+    assert len(H["history"]) == len(want)
+    for r, w in enumerate(want):
+        got = H["history"][r]
+        assert list(got["client_states"]) == w["clients"], (name, r)
+        for c, fv, snd in zip(w["clients"], w["approximate_f_value"], w["send_scalars_to_master"]):
+            cs = got["client_states"][c]["client_state"]
+            np.testing.assert_allclose(cs["approximate_f_value"], fv, rtol=rel, err_msg=f"{name} r{r} c{c} f")
+            assert cs["stats"]["send_scalars_to_master"] == snd, (name, r, c)
+        for k in ("grad_sgd_server_l2", "x_before_round", "approximate_f_avg_value"):
+            assert abs(got[k] - w[k]) <= rel * abs(w[k]), (name, r, k, got[k], w[k])

@@ -1,0 +1,74 @@
+"""The round harness on the product path (HIP codecs + HIP fold) against the reference's runs.
+
+Config C1 (FedAvg + ident, 4 clients, the "dense" MLP, D = 2465) and the DCGD runs (randk:10%,
+qsgd:10, topk:5%, plus partial participation with 2 local steps), captured from the real
+reference by tests/golden/make_golden_harness.py, replayed through flpytorch_amd.harness:
+  * device "cpu"  — the reference's --gpu -1 setting: the model side on the host, every codec call
+    and the server fold in libflcodec.so (rows cross to the GPU and back);
+  * device "cuda" — the whole round on the MI355X (the model side in torch on the GPU).
+Bar: per round grad_sgd_server_l2, x_before_round and approximate_f_avg_value
+within 1e-6 relative of the reference, the clients' f values and wire counts likewise, the
+sampling / pattern draw order exact; and every round's fold bit-exact against the oracle's
+sequential serverGradient on the harness's own client models (compat-mode patterns).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import codecs as oc
+from tests.harness_cases import DATA, META, RUN_NAMES, check_history, simulation
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ag():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    from flpytorch_amd import aggregation
+    return aggregation
+
+
+@pytest.mark.parametrize("device", ["cpu", "cuda"])
+@pytest.mark.parametrize("name", RUN_NAMES)
+def test_harness_reproduces_reference_run(ag, name, device):
+    folds = []
+    default_fold = ag.serverGradientMaster if META[name]["algorithm"] == "dcgd" else ag.serverGradientPlain
+
+    def recording_fold(buf, clients, model, x, H):
+        rows = [buf.get(i)["model"].detach().cpu().numpy().copy() for i in range(clients)]
+        gs = default_fold(buf, clients, model, x, H)
+        folds.append((x.detach().cpu().numpy().copy(), rows, gs.detach().cpu().numpy().copy()))
+        return gs
+    sim = simulation(name, device, server_gradient=recording_fold, record_iterates=True)
+    H = sim.run()
+    check_history(name, H, rel=1e-6)
+    for r in range(META[name]["rounds"]):
+        np.testing.assert_allclose(sim.iterates[r].numpy(), DATA[f"{name}_iterates"][r], rtol=1e-5, atol=1e-6,
+                                   err_msg=f"{name} round {r}")
+    # the HIP fold of each round, bit for bit the reference's sequential fp32 loop
+    for x, rows, gs in folds:
+        want = oc.server_gradient(x, rows)
+        assert np.array_equal(gs.view(np.uint32), want.view(np.uint32))
+
+
+def test_harness_patterns_are_the_reference_draws(ag):
+    """DCGD randk: the index sets the harness draws for each client (generateCompressPattern on the
+    shared stream, then the seed draw) are the reference run's own (runs.npz, make_golden.py)."""
+    from tests.golden_io import load
+    _, runs = load("runs")
+    sim = simulation("dcgd_randk10", "cpu")
+    drawn = []
+    orig = ag.Compressor.generateCompressPattern
+
+    def spy(self, rndgen, device, clientId, H):
+        orig(self, rndgen, device, clientId, H)
+        drawn.append(self.S.cpu().numpy().copy())
+    ag.Compressor.generateCompressPattern = spy
+    try:
+        sim.run()
+    finally:
+        ag.Compressor.generateCompressPattern = orig
+    want = runs["dcgd_randk10_patterns"]
+    assert len(drawn) == len(want)
+    for a, b in zip(drawn, want):
+        assert np.array_equal(a, b)

@@ -1,0 +1,104 @@
+"""CPU tests of the round harness (flpytorch_amd/harness.py) — its orchestration, not the kernels.
+
+The harness is driven with test doubles of the codec and fold protocols backed by the ORACLE
+(oracle/codecs.py: the reference's compressVector / serverGradient restated op for op), so the
+sampling order, the per-client pattern + seed draws on the shared stream, the local SGD step and the
+history scalars are checked here against the reference's own runs (tests/golden/harness.json, from
+make_golden_harness.py).  The product path (HIP codecs + HIP fold) is tests/test_gpu_harness.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import codecs as oc
+from tests.harness_cases import DATA, META, RUN_NAMES, check_history, simulation
+
+
+class OracleCompressorDouble:
+    """The reference's Compressor protocol over the oracle (CPU tensors in and out)."""
+
+    def __init__(self, spec, D):
+        self.o = oc.OracleCompressor(spec, D)
+        self.last_need_to_send_advance = 0
+
+    def isUnbiasedCompressor(self):
+        return hasattr(self.o, "w")
+
+    def isContractionCompressor(self):
+        return hasattr(self.o, "alpha")
+
+    def getW(self):
+        return self.o.w
+
+    def getAlphaContraction(self):
+        return self.o.alpha
+
+    def generateCompressPattern(self, rndgen, device, clientId, H):
+        self.o.generate(rndgen)
+
+    def compressVector(self, x):
+        out = self.o.compress(x.detach().cpu().numpy())
+        self.last_need_to_send_advance = self.o.last_need_to_send_advance
+        return torch.from_numpy(np.ascontiguousarray(out))
+
+
+def oracle_server_gradient(buf, clients, model, x, H):
+    rows, w = [], []
+    for i in range(clients):
+        buf.waitForItem()
+        r = buf.get(i)
+        rows.append(r["model"].cpu().numpy())
+        w.append(r["client_state"]["weight"])
+    return torch.from_numpy(oc.server_gradient(x.cpu().numpy(), rows, w))
+
+
+@pytest.mark.parametrize("name", RUN_NAMES)
+def test_harness_replays_reference_runs(name):
+    sim = simulation(name, "cpu", init_compressor=OracleCompressorDouble, server_gradient=oracle_server_gradient,
+                     record_iterates=True)
+    H = sim.run()
+    check_history(name, H)
+    # the iterate after every round's global step
+    for r in range(META[name]["rounds"]):
+        np.testing.assert_allclose(sim.iterates[r].numpy(), DATA[f"{name}_iterates"][r], rtol=1e-6, atol=1e-7,
+                                   err_msg=f"{name} round {r}")
+
+
+def test_sampling_matches_numpy_stream():
+    from flpytorch_amd import harness
+    rs, ref = np.random.RandomState(456), np.random.RandomState(456)
+    got = harness.get_sampled_clients(10, 3, 5, rs)
+    want = [ref.choice(10, 3, replace=False) for _ in range(5)]
+    assert all(np.array_equal(a, b) for a, b in zip(got, want))
+    rs, ref = np.random.RandomState(9), np.random.RandomState(9)
+    got = harness.get_sampled_clients(6, None, 4, rs, sampling="poisson", poisson_p=0.3)
+    want = [np.asarray([j for j in range(6) if ref.uniform() < 0.3]) for _ in range(4)]
+    assert all(np.array_equal(a, b) for a, b in zip(got, want))
+    with pytest.raises(AssertionError):
+        harness.get_sampled_clients(6, 2, 1, rs, sampling="stratified")
+
+
+def test_dense_model_gradient_matches_autograd_module():
+    """DenseModel on a flat vector == the reference's nn.Sequential "dense" model
+    (model_funcs.py:170-189) with MSELoss(sum) * (1 / n), through mutils-style flattening."""
+    from flpytorch_amd import harness
+    A, B = DATA["data_A"], DATA["data_B"]
+    m = harness.DenseModel(A, B, 16)
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Flatten(1), torch.nn.Linear(8, 32), torch.nn.ReLU(), torch.nn.Linear(32, 64),
+                              torch.nn.ReLU(), torch.nn.Linear(64, 1), torch.nn.Sigmoid())
+    x = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+    xb, yb = torch.from_numpy(A[16:32]), torch.from_numpy(B[16:32])
+    loss = torch.nn.MSELoss(reduction="sum")(net(xb), yb) * (1.0 / 16)
+    loss.backward()
+    g_ref = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+    f, g = m.value_and_gradient(x, 1)
+    assert f == (torch.zeros(1) + loss.detach()).item()
+    assert torch.equal(g, g_ref)
+
+
+def test_rejects_other_algorithms():
+    from flpytorch_amd import harness
+    m = harness.DenseModel(DATA["data_A"], DATA["data_B"], 16)
+    with pytest.raises(ValueError):
+        harness.Simulation("diana", "ident", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu")

@@ -213,3 +213,48 @@ def test_wire_format_lossless_on_reference_outputs(i):
         np.testing.assert_array_equal(wire.unpack(comp, pl, m["D"]).view(np.uint32), out.view(np.uint32))
         if m["type"] == 5 and comp.s <= 127:
             assert pl.size <= 16 + m["D"] + 15                   # one byte per element
+
+
+@pytest.mark.parametrize("i", [i for i, m in enumerate(CODEC_META) if m["type"] == 5])
+def test_dithering_closed_form_on_reference_outputs(i, monkeypatch):
+    """The closed form the oracle uses above LOOP_MAX_D (oc.dither_levels) reproduces the
+    reference's outputs bit for bit too (forced here at the fixtures' sizes)."""
+    monkeypatch.setattr(oc, "LOOP_MAX_D", 0)
+    m, X, OUT = _case(i)
+    rs = OracleRandomState(m["seed"])
+    pn = CODEC[f"c{i:02d}_pnorm"]
+    for c in range(m["n_clients"]):
+        comp = oc.OracleCompressor(m["spec"], m["D"])
+        comp.generate(rs)
+        rs.randint31()
+        out = comp.compress(X[c], pnorm=pn[c])
+        np.testing.assert_array_equal(out.view(np.uint32), OUT[c].view(np.uint32))
+
+
+@pytest.mark.parametrize("spec", ["qsgd:127", "qsgd:4", "std.dithering:10:2", "std.dithering:7:1", "terngrad",
+                                  "std.dithering:300:2"])
+def test_dithering_closed_form_equals_loop(spec):
+    """oc.dither_levels == the level loop of compressors.py:284-291 on inputs that hit every level
+    exactly (boundaries are where the loop's later interval overwrites), zeros, the max element
+    (y == 1), y just above 1 (a norm rounded below |x|), NaN and inf."""
+    g = np.random.default_rng(abs(hash(spec)) % 2 ** 32)
+    d = 50_000
+    comp = oc.OracleCompressor(spec, d)
+    lv = comp.levels
+    y = g.random(d).astype(np.float32)
+    y[: lv.size] = lv                                           # exact level hits
+    y[lv.size: 2 * lv.size] = np.nextafter(lv, np.float32(2))   # one ulp above each level
+    y[2 * lv.size: 3 * lv.size] = np.nextafter(lv, np.float32(-1))
+    y[-1], y[-2], y[-3], y[-4] = 1.0, np.nextafter(np.float32(1), np.float32(2)), np.nan, np.inf
+    u = g.random(d)
+    u[: lv.size] = 0.0
+    loop = np.zeros_like(y)
+    with np.errstate(all="ignore"):
+        for s in range(len(lv) - 1):
+            c12 = (y >= lv[s]) & (y <= lv[s + 1])
+            p = (y - lv[s + 1]) / (lv[s] - lv[s + 1])
+            c3 = u < p.astype(np.float64)
+            loop[c12 & c3] = lv[s]
+            loop[c12 & ~c3] = lv[s + 1]
+        fast = oc.dither_levels(y, u, lv)
+    np.testing.assert_array_equal(fast.view(np.uint32), loop.view(np.uint32))
