@@ -25,7 +25,8 @@ roofline: the dominant kernel's algorithmic bytes per step / its summed launch t
 with HIP events on its launch stream inside the timed region (flc_profile_*); peak 8.0 TB/s
 (MI355X_MICROARCH.md).  traffic: HBM bytes per launch from rocprofv3 PMC passes
 (profiles/pmc_<workload>.json, written by profiles/collect_pmc.py), or null.
-cpu_baseline: the oracle (numpy restatement of the reference path) timed on this host, rank 0.
+cpu_baseline: the reference's CPU uplink (oracle/torch_cpu.py: its torch / numpy calls) timed on
+this host's cores, rank 0, pattern / compress / fold separately.
 """
 import argparse
 import json
@@ -43,12 +44,12 @@ sys.path.insert(0, ROOT)
 PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
 
 WORKLOADS = {
-    "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2,
+    "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2, n_total=1024,
                others=["k_topk_sample", "k_cand_select", "k_chunk_accum"]),
-    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_coarse", config=1,
+    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_coarse", config=1, n_total=256,
                others=["k_chunk_accum"]),
     # sparse QSGD path (dither_sparse.hip): one read of every row in k_ds_filter
-    "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3,
+    "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3, n_total=4096,
                others=["k_ds_sample", "k_ds_accum"]),
     # C5: mixed per-client codec (client i -> specs[i % 3]); a pool of resident distinct rows is
     # replayed through the clients' row pointers (819 GB of distinct rows per GPU would not fit)
@@ -56,7 +57,7 @@ WORKLOADS = {
                kernel="k_ds_filter", config=4,
                others=["k_topk_filter", "k_randk_coarse", "k_randk_fine", "k_ds_accum", "k_chunk_accum"]),
     # the serverGradient fold alone (identity codec), C4's shard shape
-    "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3, others=[]),
+    "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3, n_total=4096, others=[]),
 }
 
 
@@ -83,27 +84,26 @@ def kernel_bytes(kernel, n, d, k):
     return 4 * n * d                # k_topk_filter / k_ds_filter: read every row once
 
 
-def cpu_baseline(spec, d, budget_s=12.0, specs=None):
-    """Oracle (numpy, 1 core) encode + sequential reduce of a bounded sample of rows (mixed: the
-    rows cycle through the constituent codecs like the clients do)."""
-    from oracle import codecs as oc
-    from oracle.rng import OracleRandomState
-    g = np.random.default_rng(0)
-    rs = OracleRandomState(123)
-    t0 = time.perf_counter()
-    rows = 0
-    acc = None
-    while True:
-        x = g.standard_normal(d).astype(np.float32)
-        o = oc.OracleCompressor(specs[rows % len(specs)] if specs else spec, d)
-        o.generate(rs)
-        rs.randint31()
-        e = o.compress(x)
-        acc = e if acc is None else acc + e
-        rows += 1
-        if time.perf_counter() - t0 > budget_s or rows >= 64:
-            break
-    dt = time.perf_counter() - t0
+def cpu_baseline(spec, d, n_job, budget_s=10.0, specs=None):
+    """The reference's CPU uplink on this host: oracle/torch_cpu.py issues the
+    reference's own torch / numpy calls (generateCompressPattern, compressVector, serverGradient's
+    fold) on CPU tensors, with torch's intra-op threads = the host cores this job may use.  Phases
+    timed separately per client over a bounded sample (about budget_s of work); `value` is the
+    metric's algorithmic bytes of the sample / the sample's pattern + compress + fold time, and the
+    time for the bench's N clients is extrapolated linearly (labelled)."""
+    from oracle.torch_cpu import time_uplink
+    affinity = len(os.sched_getaffinity(0))
+    # the job's CPU share: OMP_NUM_THREADS when the launcher sets it (16 per GPU on the MI355X
+    # boxes, whose affinity mask shows the whole machine), else every CPU in the affinity mask
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS") or affinity))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        r = time_uplink(specs or [spec], d, budget_s)
+    finally:
+        torch.set_num_threads(prev)
+    n = r["clients"]
+    t = r["pattern_s"] + r["compress_s"] + r["fold_s"]
     k = math.ceil(0.01 * d)
     cpu_model = None
     try:
@@ -111,13 +111,19 @@ def cpu_baseline(spec, d, budget_s=12.0, specs=None):
             cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
     except OSError:
         pass
-    return {"value": round(algorithmic_bytes(spec, rows, d, k, specs) / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+    per = {ph: round(r[ph + "_s"] / n * 1e3, 3) for ph in ("pattern", "compress", "fold")}
+    return {"value": round(algorithmic_bytes(spec, n, d, k, specs) / t / 1e9, 4), "unit": "GB/s", "cores": threads,
             "kind": "port",
+            "ms_per_client": per,
+            "value_encode_fold_only": round(algorithmic_bytes(spec, n, d, k, specs) /
+                                            (r["compress_s"] + r["fold_s"]) / 1e9, 4),
+            "extrapolated_s_for_bench_N": {"clients": n_job, "seconds": round(t / n * n_job, 1),
+                                           "note": "linear in clients (labelled extrapolation)"},
             # the host the baseline ran on
-            "host": {"cpu_model": cpu_model, "affinity_cpus": len(os.sched_getaffinity(0)),
-                     "torch_threads": torch.get_num_threads()},
-            "sample": f"oracle/codecs.py {'/'.join(specs) if specs else spec}: pattern + encode + sequential fp32 reduce of {rows} rows x D={d} "
-                      f"({dt:.1f} s, numpy single-threaded)"}
+            "host": {"cpu_model": cpu_model, "affinity_cpus": affinity, "torch_threads": threads},
+            "sample": f"oracle/torch_cpu.py (the reference's torch calls) "
+                      f"{'/'.join(specs) if specs else spec}: numpy-stream patterns, compressVector, "
+                      f"serverGradient fold of {n} clients x D={d} ({t:.1f} s, {threads} torch threads)"}
 
 
 def e2e(args):
@@ -353,6 +359,12 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--compat", action="store_true",
+                    help="compat-mode patterns: the reference's numpy-stream RandK indices / dithering uniforms, "
+                         "resident in HBM and read by the kernels (their bytes counted)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: N clients per GPU; strong: the workload's fixed round size (C4: N=4096) in 8 "
+                         "fixed client blocks over the GPUs, combined in block order (G-invariant)")
     ap.add_argument("--dropin", action="store_true",
                     help="per-client compressVector + serverGradient fold (the install() path) vs the fused uplink")
     ap.add_argument("--wire", action="store_true",
@@ -395,14 +407,72 @@ def main():
     specs = wl.get("specs")
     mixed = specs is not None
     k = math.ceil(0.01 * d) if mixed else (getattr(ag.initCompressor(spec, d), "K", 0) or 0)
+    strong = args.scaling == "strong"
+    if strong:
+        # fixed N for every G: the round's n_total clients in 8 fixed blocks,
+        # rank r of G owns blocks r*8/G ..; each block folded into its own exact partial, the 8
+        # partials combined in block order (G-invariant bits).  A rank holds its clients' rows when
+        # they fit (160 GB), else one block's rows, replayed for every block it owns (each block
+        # with its own client ids, hence its own device-RNG draws) — C4's 1-GPU point replays the
+        # resident 512-row shard 8x
+        if mixed:
+            raise SystemExit("--scaling strong: not for the mixed workload (c5)")
+        from flpytorch_amd.sharding import N_BLOCKS, ShardedUplink, product_fold, product_partial, rank_clients
+        n_total = wl["n_total"] if not args.n else args.n
+        r_lo, r_hi = rank_clients(n_total, world, rank)
+        n = r_hi - r_lo
+        block = -(-n_total // N_BLOCKS)
+        replay = n * d * 4 > 160e9
+        n_dist = block if replay else n
     # synthetic rows ~ N(0, 1) fp32, seeded per rank (device generator; never leaves HBM)
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    n_dist = min(n, wl["pool"]) if mixed else n
+    if not strong:
+        n_dist = min(n, wl["pool"]) if mixed else n
     rows = torch.empty((n_dist, d), dtype=torch.float32, device=dev)
     for i in range(0, n_dist, 64):
         rows[i:i + 64].normal_(generator=gen)
     out = torch.empty(d, dtype=torch.float32, device=dev)
     client0 = rank * n
+    compat_kw, compat_bytes, compat_note = {}, 0, None
+    if args.compat and not spec.startswith("randk"):
+        # float64 uniforms go through the dense two-pass dithering path (norm pass, then the encode
+        # pass reading row + uniforms): the encode pass is the dominant kernel
+        wl["kernel"], wl["others"] = "k_ew_accum_vec", ["k_norm_partials"]
+    if args.compat:
+        # compat mode: the reference's numpy-stream patterns, drawn on the host (the
+        # C++ MT19937 restatement, bit-exact) before the timed region and resident in HBM; the
+        # kernels read them: RandK int64 indices (+8 N K bytes), dithering float64 uniforms (+8 N D)
+        if world > 1 or mixed or strong:
+            raise SystemExit("--compat: single-GPU, single-codec workloads")
+        rs = np.random.RandomState(123)
+        t0 = time.perf_counter()
+        if spec.startswith("randk"):
+            idx = np.empty((n, k), dtype=np.int64)
+            for i in range(n):
+                idx[i] = ag.stream_choice(rs, d, k)
+                ag.stream_randint31(rs)
+            compat_kw["randk_idx"] = torch.from_numpy(idx).to(dev)
+            compat_bytes = 8 * n * k
+            compat_note = f"host numpy-stream choice(D, K) for {n} clients: {(time.perf_counter() - t0) * 1e3:.0f} ms"
+        elif spec.startswith(("qsgd", "std_dithering", "natural", "terngrad")):
+            # float64 uniforms of `pool` clients drawn from the stream, replicated over the N rows
+            # (N x D x 8 B resident; the numbers do not change the kernels' work)
+            pool = min(n, 16)
+            uni = torch.empty((n, d), dtype=torch.float64, device=dev)
+            host = np.empty(d, dtype=np.float64)
+            for i in range(pool):
+                ag.stream_rand(rs, d, out=host)
+                ag.stream_randint31(rs)
+                uni[i].copy_(torch.from_numpy(host))
+            for i in range(pool, n):
+                uni[i].copy_(uni[i % pool])
+            compat_kw["uniforms"] = uni
+            compat_bytes = 8 * n * d
+            compat_note = (f"host numpy-stream rand(D) for {pool} clients ({(time.perf_counter() - t0) / pool * 1e3:.0f} "
+                           f"ms per client), replicated over the {n} rows")
+        else:
+            raise SystemExit(f"--compat: {spec} draws no pattern")
+        torch.cuda.synchronize()
     if mixed:
         row_list = [rows[i % n_dist] for i in range(n)]
         up = ag.MixedUplink(specs, d, seed=20241015, device=dev)
@@ -412,17 +482,25 @@ def main():
     else:
         red = ag.UplinkReducer(ag.initCompressor(spec, d), device=dev, seed=20241015)
 
-    if world > 1 and not mixed:
+    if strong:
+        uplink = ShardedUplink(product_partial(red), group=dist.group.WORLD if world > 1 else None, mode="ordered",
+                               fold=product_fold())
+
+        def rows_of(b_lo, b_hi):
+            return rows[:b_hi - b_lo] if replay else rows[b_lo - r_lo:b_hi - r_lo]
+    elif world > 1 and not mixed:
         from flpytorch_amd.sharding import ShardedUplink, product_partial
         # local partial = sum_i C_i(row_i) in client order (fp32 divisor 1.0 keeps it exact),
         # one RCCL all-reduce of D floats over xGMI, then the global mean
         uplink = ShardedUplink(product_partial(red), mode="allreduce")
 
     def step():
-        if mixed:
+        if strong:
+            uplink(rows_of, client0=r_lo, total_weight=float(n_total), n_clients=n_total, out=out, d=d, device=dev)
+        elif mixed:
             up(row_list, client0=client0, total_weight=float(n * world), out=out, group=group)
         elif world == 1:
-            red(rows, out=out, client0=client0)
+            red(rows, out=out, client0=client0, **compat_kw)
         else:
             uplink(rows, client0=client0, total_weight=float(n * world), out=out)
 
@@ -455,12 +533,14 @@ def main():
         elapsed = float(t.item())
 
     step_ms = elapsed / args.steps * 1e3
-    total_bytes = algorithmic_bytes(spec, n, d, k, specs) * world
+    total_bytes = algorithmic_bytes(spec, n_total, d, k) if strong else algorithmic_bytes(spec, n, d, k, specs) * world
+    total_bytes += compat_bytes
     value = total_bytes / (elapsed / args.steps) / 1e9
     # the dominant kernel may run as several launches per step (sparse QSGD: one per row group):
     # its achieved rate is the algorithmic bytes of a step over its summed launch time per step
     # mixed: the dominant kernel serves the qsgd group only
     kb = kernel_bytes(wl["kernel"], len(range(specs.index("qsgd:127"), n, len(specs))) if mixed else n, d, k)
+    kb += compat_bytes                     # the dominant kernel reads the resident compat patterns
     kavg_ms = kms / max(klaunch, 1)
     kstep_ms = kms / args.steps
     achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
@@ -471,7 +551,8 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d, budget_s=20.0 if mixed else 12.0, specs=specs)
+        cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d, n_total if strong else n * world,
+                                                             budget_s=15.0 if mixed else 10.0, specs=specs)
         line = {
             "metric": "gradient-codec encode+reduce GB/s (device-resident), [N,D] fp32; % HBM peak",
             "value": round(value, 2),
@@ -481,16 +562,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(step_ms, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic N(0,1) fp32 rows generated on device (seeded per rank); device-RNG patterns"
+            "data": "synthetic N(0,1) fp32 rows generated on device (seeded per rank); "
+                    + (f"compat patterns (the reference's numpy stream, resident in HBM; {compat_note})"
+                       if args.compat else "device-RNG patterns")
                     + (f"; {n_dist} resident distinct rows replayed through the {n} clients' row pointers, "
-                       "each client its own codec (client id mod 3) and device-RNG key" if mixed else ""),
-            "config": {"workload": f"C{wl['config'] + 1} {'/'.join(specs) if mixed else spec} N={n}/GPU D={d}",
+                       "each client its own codec (client id mod 3) and device-RNG key" if mixed else "")
+                    + (f"; strong scaling: {n_total} clients in {N_BLOCKS} fixed blocks, {n} on this GPU"
+                       + (f", one block's {n_dist} rows resident and replayed for each of its blocks (own client ids)"
+                          if replay else ", all resident") if strong else ""),
+            "config": {"workload": (f"C{wl['config'] + 1} {spec} N={n_total} (fixed) D={d}" if strong else
+                                    f"C{wl['config'] + 1} {'/'.join(specs) if mixed else spec} N={n}/GPU D={d}"),
                        "codec": "/".join(specs) if mixed else spec,
-                       "clients_per_gpu": n, "clients_total": n * world, "D": d, "K": k,
-                       "parallelism": f"client-shard dp{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+                       "clients_per_gpu": n, "clients_total": n_total if strong else n * world, "D": d, "K": k,
+                       "parallelism": f"client-shard dp{world}" + (
+                           f" + {N_BLOCKS} block partials, all-to-all + block-order fold + all-gather (G-invariant)"
+                           if strong else (" + RCCL all-reduce" if world > 1 else ""))},
             "pct_hbm_peak": round(100.0 * value / world / PEAK_GBS, 2),
             # RandK also reports the dense-equivalent rate 4 N D / t (never the roofline)
             "dense_equivalent_GBps": round((4 * n * d + 4 * d) * world / (elapsed / args.steps) / 1e9, 1)

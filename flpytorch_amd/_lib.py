@@ -35,6 +35,7 @@ EXPORTS = [
     "flc_payload_bytes", "flc_payload_format", "flc_pack_workspace_size", "flc_pack", "flc_unpack",
     "flc_unpack_reduce_workspace_size", "flc_unpack_reduce",
     "flc_combine_workspace_size", "flc_combine_partials",
+    "flc_combine_blocks_workspace_size", "flc_combine_blocks",
     "flc_mt_choice", "flc_mt_rand", "flc_mt_randint31",
     "flc_device_uniform", "flc_device_randk_indices",
     "flc_profile_enable", "flc_profile_collect",
@@ -118,6 +119,9 @@ def load():
         lib.flc_combine_workspace_size.argtypes = [vp, i64, i32]
         lib.flc_combine_workspace_size.restype = sz
         lib.flc_combine_partials.argtypes = [vp, vp, i64, f32, i32, vp, sz, vp]
+        lib.flc_combine_blocks_workspace_size.argtypes = [vp, i64, i64]
+        lib.flc_combine_blocks_workspace_size.restype = sz
+        lib.flc_combine_blocks.argtypes = [vp, vp, i64, i64, i64, f32, vp, vp, sz, vp]
         lib.flc_mt_choice.argtypes = [vp, vp, i64, i64, vp, vp]
         lib.flc_mt_rand.argtypes = [vp, vp, i64, vp]
         lib.flc_mt_randint31.argtypes = [vp, vp, i64, vp]
@@ -131,7 +135,8 @@ def load():
             if name not in ("flc_version", "flc_last_error_string", "flc_device_uniform",
                             "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
                             "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",
-                            "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size"):
+                            "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size",
+                            "flc_combine_blocks_workspace_size"):
                 getattr(lib, name).restype = i32
         _lib = lib
         return lib

@@ -37,12 +37,14 @@ def _work_device(t):
     return t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
 
 
-def reduce_rows(x, rows, weights=None, relative=True, out=None):
+def reduce_rows(x, rows, weights=None, relative=True, out=None, divisor=None):
     """out = (sum_i w_i * (x - rows_i)) / sum(w)   (relative=True, client models in)
        out = (sum_i w_i * rows_i) / sum(w)         (relative=False, client updates in)
 
     ``rows`` is a list of fp32 device tensors shaped like ``x`` (or a 2-D [N, D] tensor), on
     ``x``'s device; ``x`` must be a device tensor (the callers move host tensors first).
+    ``divisor`` replaces the fp32 divisor sum(w) (the multi-GPU block fold divides the sum of the
+    block partials by the global client weight).
     """
     _lib.require_gpu()
     lib = _lib.load()
@@ -57,6 +59,8 @@ def reduce_rows(x, rows, weights=None, relative=True, out=None):
         return out.zero_()
     weights = [1.0] * n if weights is None else [float(w) for w in weights]
     uniform, total = _weights_and_total(weights)
+    if divisor is not None:
+        total = float(divisor)
     keep = []
     w_ptr = None
     if not uniform:

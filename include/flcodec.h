@@ -223,6 +223,18 @@ size_t flc_combine_workspace_size(void* rccl_comm, int64_t d, int mode);
 int flc_combine_partials(void* rccl_comm, float* d_partial, int64_t d, float w_total, int mode,
                          void* d_ws, size_t ws_bytes, void* stream);
 
+/* G-invariant combine (SURVEY §8e "combine the 8 block partials in fixed order"): the round's
+ * clients fall into fixed contiguous blocks (8 in flpytorch_amd.sharding), split evenly over the
+ * ranks in rank order; d_blocks holds this rank's nb_local exact block partials (rows ld floats
+ * apart, block order).  On return every rank's d_out = (((B_0 + B_1) + ...) + B_last) / w_total
+ * over ALL blocks — the same bits for any rank count.  All-to-all of column slices (grouped
+ * ncclSend/ncclRecv), a block-order fold of the rank's slice, ncclAllGather: per rank
+ * ~2 (G-1)/G x 4 D bytes with one block per rank.  Every rank must pass the same nb_local and d.
+ * Replaces the same reference code as flc_combine_partials. */
+size_t flc_combine_blocks_workspace_size(void* rccl_comm, int64_t nb_local, int64_t d);
+int flc_combine_blocks(void* rccl_comm, const float* d_blocks, int64_t ld, int64_t nb_local, int64_t d,
+                       float w_total, float* d_out, void* d_ws, size_t ws_bytes, void* stream);
+
 /* ----------------------------------------------------------------------------------------
  * Host side of compat mode: the numpy legacy MT19937 stream (what the reference's
  * rndgen.choice / rand / random / randint draw, compressors.py:204-212, algorithms.py:2055),

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from flpytorch_amd.sharding import ShardedUplink, client_block
+from flpytorch_amd.sharding import N_BLOCKS, ShardedUplink, client_block, rank_blocks, rank_clients
 from oracle import codecs as oc
 
 
@@ -47,52 +47,110 @@ def oracle_partial(spec, d):
     return run
 
 
-def _worker(rank, world, port, spec, n, d, mode, q):
+def torch_fold(stack, total):
+    """The block fold's contract in torch-CPU: sequential fp32 sum in block order, true division."""
+    acc = stack[0].clone()
+    for b in range(1, stack.shape[0]):
+        acc.add_(stack[b])
+    return acc.div_(torch.tensor(float(total), dtype=torch.float32))
+
+
+def _worker(rank, world, port, spec, n, d, mode, replay, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rows = make_rows(n, d)
-    lo, hi = client_block(n, world, rank)
-    up = ShardedUplink(oracle_partial(spec, d), mode=mode)
-    out = up(torch.from_numpy(rows[lo:hi].copy()), client0=lo, total_weight=float(n))
+    if mode == "ordered":
+        lo, hi = rank_clients(n, world, rank)
+        up = ShardedUplink(oracle_partial(spec, d), mode=mode, fold=torch_fold)
+        if replay:
+            out = up(lambda a, b: torch.from_numpy(rows[a:b].copy()), client0=lo, total_weight=float(n), n_clients=n,
+                     d=d, device="cpu")
+        else:
+            out = up(torch.from_numpy(rows[lo:hi].copy()), client0=lo, total_weight=float(n), n_clients=n)
+    else:
+        lo, hi = client_block(n, world, rank)
+        up = ShardedUplink(oracle_partial(spec, d), mode=mode)
+        out = up(torch.from_numpy(rows[lo:hi].copy()), client0=lo, total_weight=float(n))
     q.put((rank, out.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("mode", ["allreduce", "ordered"])
-@pytest.mark.parametrize("spec", ["topk:5%", "ident"])
-def test_sharded_uplink_matches_single_process(world, mode, spec):
-    n, d = 7, 4099
+def _run(world, spec, n, d, mode, replay=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, spec, n, d, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, spec, n, d, mode, replay, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("spec", ["topk:5%", "ident"])
+def test_sharded_uplink_matches_single_process(world, spec):
+    n, d = 7, 4099
+    res = _run(world, spec, n, d, "allreduce")
     rows = make_rows(n, d)
     enc = [oc.OracleCompressor(spec, d).compress(rows[i]) for i in range(n)]
     want = oc.reduce_plain(enc)
     for r in range(world):
         np.testing.assert_array_equal(res[r], res[0])            # every rank holds the same result
         np.testing.assert_allclose(res[r], want, rtol=2e-6, atol=1e-7)
-    if mode == "ordered":
-        # fixed fold: (block0 + block1 + ...) / n, reproducible
-        parts = []
+
+
+def block_fold_want(spec, n, d):
+    """(((B_0 + B_1) + ...) + B_7) / n with B_b the client-order sum of block b's encodings."""
+    rows = make_rows(n, d)
+    enc = [oc.OracleCompressor(spec, d).compress(rows[i]) for i in range(n)]
+    parts = []
+    for b in range(N_BLOCKS):
+        lo, hi = client_block(n, N_BLOCKS, b)
+        acc = np.zeros(d, np.float32) if hi == lo else enc[lo].copy()
+        for e in enc[lo + 1:hi]:
+            acc = acc + e
+        parts.append(acc)
+    fold = parts[0].copy()
+    for p in parts[1:]:
+        fold = fold + p
+    return fold / np.float32(n)
+
+
+@pytest.mark.parametrize("spec,n,d", [("topk:5%", 37, 4099), ("ident", 5, 1021), ("ident", 64, 1)])
+def test_ordered_mode_is_g_invariant(spec, n, d):
+    """the 8 fixed client-block partials folded in block order — G = 1, 2, 4, 8 give
+    the same bits on every rank, equal to the stated fold (n = 5: blocks 5..7 empty)."""
+    want = block_fold_want(spec, n, d)
+    for world in (1, 2, 4, 8):
+        res = _run(world, spec, n, d, "ordered")
         for r in range(world):
-            lo, hi = client_block(n, world, r)
-            acc = enc[lo].copy()
-            for e in enc[lo + 1:hi]:
-                acc = acc + e
-            parts.append(acc)
-        fold = parts[0].copy()
-        for p in parts[1:]:
-            fold = fold + p
-        np.testing.assert_array_equal(res[0], fold / np.float32(n))
+            assert np.array_equal(res[r].view(np.uint32), want.view(np.uint32)), (world, r)
+
+
+def test_ordered_mode_replayed_rows():
+    """The strong-scaling bench's form: rows(lo, hi) called per block."""
+    spec, n, d = "topk:5%", 16, 2053
+    want = block_fold_want(spec, n, d)
+    res = _run(2, spec, n, d, "ordered", True)
+    for r in range(2):
+        assert np.array_equal(res[r].view(np.uint32), want.view(np.uint32))
+
+
+def test_rank_blocks_and_clients():
+    assert [list(rank_blocks(4, r)) for r in range(4)] == [[0, 1], [2, 3], [4, 5], [6, 7]]
+    with pytest.raises(ValueError):
+        rank_blocks(3, 0)
+    for n in (0, 5, 37, 4096):
+        for world in (1, 2, 4, 8):
+            spans = [rank_clients(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    with pytest.raises(ValueError):
+        ShardedUplink(lambda *a: None, mode="ordered")
 
 
 @pytest.mark.parametrize("n,world", [(7, 2), (8, 8), (3, 4), (4096, 8), (1, 1)])

@@ -239,3 +239,39 @@ print(json.dumps(names))
     ref_names = set(json.loads(r.stdout.strip().splitlines()[-1]))
     ours = set(ag.PLAIN_FOLD) | set(ag.MASTER_FOLD) | set(ag.SHIFTED_FOLD) | {"FRECON"}
     assert ours == ref_names, (sorted(ours ^ ref_names))
+
+
+@pytest.mark.parametrize("spec", ["topk:1%", "randk:1%", "qsgd:127", "qsgd:4", "ident"])
+def test_torch_cpu_baseline_matches_oracle(spec):
+    """oracle/torch_cpu.py (the reference's torch calls, timed as bench.py's cpu_baseline) computes
+    what the numpy oracle computes: same numpy-stream patterns, bit-equal outputs (dithering given
+    torch's own CPU norm), and the fold equals server_gradient."""
+    import torch
+    from oracle import codecs as oc
+    from oracle.rng import OracleRandomState
+    from oracle.torch_cpu import TorchCpuCodec, fold
+    d = 20011
+    g = np.random.default_rng(3).standard_normal((3, d)).astype(np.float32)
+    rs_t, rs_o = np.random.RandomState(77), OracleRandomState(77)
+    outs = []
+    for i in range(3):
+        t = TorchCpuCodec(spec, d)
+        t.generate(rs_t)
+        o = oc.OracleCompressor(spec, d)
+        o.generate(rs_o)
+        x = torch.from_numpy(g[i])
+        got = t.compress(x).numpy()
+        pn = float(torch.norm(x, p=2)) if spec.startswith("qsgd") else None
+        want = o.compress(g[i], pnorm=pn) if pn is not None else o.compress(g[i])
+        assert np.array_equal(got.view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
+        outs.append(got)
+    x0 = np.zeros(d, np.float32)
+    models = [x0 - e for e in outs]
+    gs = fold(torch.from_numpy(x0), [torch.from_numpy(m) for m in models]).numpy()
+    assert np.array_equal(gs.view(np.uint32), oc.server_gradient(x0, models).view(np.uint32))
+
+
+def test_torch_cpu_time_uplink_phases():
+    from oracle.torch_cpu import time_uplink
+    r = time_uplink(["randk:1%", "topk:1%", "qsgd:4"], 10007, budget_s=0.01)
+    assert r["clients"] >= 2 and all(r[k] >= 0 for k in ("pattern_s", "compress_s", "fold_s"))

@@ -24,7 +24,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL_SUBSTR = {"c3": "k_topk_filter_fast", "c4": "k_ds_filter", "reduce": "k_reduce_vec",
-                 "c2": "k_randk_scatter"}
+                 "c2": "k_randk_coarse", "c5": "k_ds_filter"}
 
 
 def run_pass(ctr, wl, extra, outdir):
