@@ -46,8 +46,8 @@ PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level paramet
 WORKLOADS = {
     "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2, n_total=1024,
                others=["k_topk_sample", "k_cand_select", "k_chunk_accum"]),
-    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_coarse", config=1, n_total=256,
-               others=["k_chunk_accum"]),
+    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_fold", config=1, n_total=256,
+               others=["k_randk_counts"]),
     # sparse QSGD path (dither_sparse.hip): one read of every row in k_ds_filter
     "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3, n_total=4096,
                others=["k_ds_sample", "k_ds_accum"]),
@@ -55,7 +55,7 @@ WORKLOADS = {
     # replayed through the clients' row pointers (819 GB of distinct rows per GPU would not fit)
     "c5": dict(spec="mixed", specs=["randk:1%", "topk:1%", "qsgd:127"], n=2048, d=100_000_000, pool=48,
                kernel="k_ds_filter", config=4,
-               others=["k_topk_filter", "k_randk_coarse", "k_randk_fine", "k_ds_accum", "k_chunk_accum"]),
+               others=["k_topk_filter", "k_randk_counts", "k_randk_fold", "k_ds_accum", "k_chunk_accum"]),
     # the serverGradient fold alone (identity codec), C4's shard shape
     "reduce": dict(spec="ident", n=512, d=25_000_000, kernel="k_reduce_vec", config=3, n_total=4096, others=[]),
 }
@@ -77,8 +77,10 @@ def algorithmic_bytes(spec, n, d, k, specs=None):
 
 def kernel_bytes(kernel, n, d, k):
     """Algorithmic bytes one launch of the dominant kernel must move."""
+    if kernel == "k_randk_fold":
+        return 4 * n * k + 4 * d    # device RandK: gather K values per row, write the [D] result
     if kernel == "k_randk_coarse":
-        return 8 * n * k            # C2 (one chunk per superchunk): sample, bucket, gather K values per row + write them
+        return 8 * n * k            # compat RandK (one chunk per superchunk): gather K values per row + write them
     if kernel in ("k_ew_accum_vec", "k_reduce_vec"):
         return 4 * n * d + 4 * d    # read every row once, write the [D] result
     return 4 * n * d                # k_topk_filter / k_ds_filter: read every row once
@@ -434,6 +436,8 @@ def main():
     out = torch.empty(d, dtype=torch.float32, device=dev)
     client0 = rank * n
     compat_kw, compat_bytes, compat_note = {}, 0, None
+    if args.compat and spec.startswith("randk"):
+        wl["kernel"], wl["others"] = "k_randk_coarse", ["k_randk_fine", "k_chunk_accum"]
     if args.compat and not spec.startswith("randk"):
         # float64 uniforms go through the dense two-pass dithering path (norm pass, then the encode
         # pass reading row + uniforms): the encode pass is the dominant kernel
@@ -544,6 +548,12 @@ def main():
     kavg_ms = kms / max(klaunch, 1)
     kstep_ms = kms / args.steps
     achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
+    line_floor = None
+    if wl["kernel"] == "k_randk_fold":
+        # sparse 4-B gathers fetch whole 128-B lines (profiles/r02/probe_gather_fetch.txt): the
+        # gather's physical floor is the expected number of distinct lines touched, x 128 B
+        nr = len(range(specs.index("randk:1%"), n, len(specs))) if mixed else n
+        line_floor = nr * (d / 32.0) * (1.0 - (1.0 - k / d) ** 32) * 128 + 4 * d
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
@@ -589,7 +599,10 @@ def main():
                          "frac": round(achieved / PEAK_GBS, 4) if achieved else None, "traffic": traffic,
                          "bytes_per_step": kb, "kernel_ms_per_step": round(kstep_ms, 4),
                          "avg_launch_ms": round(kavg_ms, 4), "launches": klaunch,
-                         "other_kernels_avg_ms": others},
+                         "other_kernels_avg_ms": others,
+                         **({"line_floor_bytes_per_step": int(line_floor),
+                             "line_floor_GBps": round(line_floor / (kstep_ms * 1e-3) / 1e9, 1) if klaunch else None}
+                            if line_floor else {})},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

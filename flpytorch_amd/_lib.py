@@ -38,6 +38,7 @@ EXPORTS = [
     "flc_combine_blocks_workspace_size", "flc_combine_blocks",
     "flc_mt_choice", "flc_mt_rand", "flc_mt_randint31",
     "flc_device_uniform", "flc_device_randk_indices",
+    "flc_device_randk_counts_workspace_size", "flc_device_randk_counts",
     "flc_profile_enable", "flc_profile_collect",
     "flc_selftest_division",
 ]
@@ -128,6 +129,9 @@ def load():
         lib.flc_device_uniform.argtypes = [ctypes.c_uint64, i64, i64]
         lib.flc_device_uniform.restype = ctypes.c_double
         lib.flc_device_randk_indices.argtypes = [ctypes.c_uint64, i64, i64, i64, vp]
+        lib.flc_device_randk_counts_workspace_size.argtypes = [i64, i64]
+        lib.flc_device_randk_counts_workspace_size.restype = sz
+        lib.flc_device_randk_counts.argtypes = [ctypes.c_uint64, i64, i64, i64, i64, vp, vp, sz, vp]
         lib.flc_profile_enable.argtypes = [i32]
         lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
         lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
@@ -136,7 +140,7 @@ def load():
                             "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
                             "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",
                             "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size",
-                            "flc_combine_blocks_workspace_size"):
+                            "flc_combine_blocks_workspace_size", "flc_device_randk_counts_workspace_size"):
                 getattr(lib, name).restype = i32
         _lib = lib
         return lib

@@ -112,7 +112,7 @@ namespace flc {
 size_t encode_row_workspace(const flc_codec_params* prm, int64_t d) {
     if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
     if (prm->codec == FLC_RANK_K) return rk_workspace(prm, 1, d, false);
-    if (prm->codec == FLC_RANDK) return 0;
+    if (prm->codec == FLC_RANDK) return randk_device_workspace(1, d);
     return ew_workspace(prm, 1, d);
 }
 }  // namespace flc
@@ -121,7 +121,7 @@ extern "C" size_t flc_encode_workspace_size(const flc_codec_params* prm, int64_t
     if (!prm || !known(prm->codec)) return 0;
     if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
     if (prm->codec == FLC_RANK_K) return rk_workspace(prm, 1, d, false);
-    if (prm->codec == FLC_RANDK) return 0;
+    if (prm->codec == FLC_RANDK) return randk_device_workspace(1, d);
     return ew_workspace(prm, 1, d);
 }
 
@@ -140,7 +140,7 @@ int encode_row(const flc_codec_params* prm, const flc_pattern* pat, const float*
     switch (prm->codec) {
         case FLC_RANDK:
             if (!(pat && pat->d_randk_idx) && prm->k > d) { set_error("randk: K > D"); return FLC_ERR_ARG; }
-            return randk_dense(prm, pat, d_x, d, d_out, st);
+            return randk_dense(prm, pat, d_x, d, d_out, d_ws, ws_bytes, st);
         case FLC_RANK_K: {
             RowSrc r{d_x, d, nullptr};
             return rk_run(prm, r, 1, d, /*reduce=*/false, nullptr, 1.f, d_out, d_ws, ws_bytes, st);
@@ -258,4 +258,18 @@ extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern*
     }
     RowSrc s{d_rows, ld, d_row_ptrs};
     return ew_run(prm, pat, s, vec, n, d, nullptr, d_pnorms_out, false, d_out, d_w, w_total, d_ws, ws_bytes, st);
+}
+
+extern "C" size_t flc_device_randk_counts_workspace_size(int64_t n, int64_t d) {
+    if (n < 1 || d < 1) return 0;
+    return randk_device_workspace(n, d);
+}
+
+extern "C" int flc_device_randk_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, int64_t k,
+                                       uint32_t* d_counts, void* d_ws, size_t ws_bytes, void* stream) {
+    if (n < 1 || d < 1 || k < 1 || k > d || d >= (int64_t)0xFFFFFFFF || !d_counts) {
+        set_error("flc_device_randk_counts: bad arguments");
+        return FLC_ERR_ARG;
+    }
+    return randk_device_counts(seed, client0, n, d, k, d_counts, d_ws, ws_bytes, (hipStream_t)stream);
 }

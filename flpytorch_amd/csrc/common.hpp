@@ -154,7 +154,11 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
 size_t rk_workspace(const flc_codec_params* prm, int64_t n, int64_t d, bool reduce);
 int rk_run(const flc_codec_params* prm, RowSrc rows, int64_t n, int64_t d, bool reduce, const float* w, float wt,
            float* out, void* wsp, size_t ws_bytes, hipStream_t st);
-int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out,
+size_t randk_device_workspace(int64_t n, int64_t d);
+int randk_device_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, int64_t k, uint32_t* cnt, void* ws,
+                        size_t ws_bytes, hipStream_t st);
+int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out, void* ws,
+                size_t ws_bytes,
                 hipStream_t st);
 
 // ------------------------------------------------------------------------------------------
@@ -227,41 +231,6 @@ __host__ __device__ inline uint32_t thr32(float p) {
 #endif
 }
 __host__ __device__ inline bool below32(uint32_t h, float p) { return h < thr32(p); }
-
-// Keyed bijection on [0, d): balanced Feistel on 2h bits (4^h >= d) with cycle walking.
-// RandK device mode takes the first K images: K distinct indices drawn uniformly.
-struct Feistel {
-    // Balanced 4-round Feistel permutation of [0, 2^(2 half_bits)) with cycle walking into [0, d):
-    // the device-RNG RandK set of a client is {perm(t) : t < K}.  Round function: fmix32 of the
-    // half XOR a 32-bit round key (round keys from the client key by mix64).
-    uint32_t rkey[4];
-    uint32_t half_bits;
-    uint32_t half_mask;
-    uint64_t d;
-    __host__ __device__ Feistel(uint64_t ckey, uint64_t dd) : d(dd) {
-        uint32_t b = 1;
-        while ((1ull << (2 * b)) < dd) ++b;
-        half_bits = b;
-        half_mask = (b >= 32) ? 0xFFFFFFFFu : ((1u << b) - 1u);
-        for (int i = 0; i < 4; ++i) rkey[i] = (uint32_t)mix64(ckey + ((uint64_t)i << 56));
-    }
-    __host__ __device__ inline uint32_t round_fn(uint32_t r, int i) const { return fmix32(r ^ rkey[i]) & half_mask; }
-    __host__ __device__ inline uint64_t once(uint64_t v) const {
-        uint32_t l = (uint32_t)(v >> half_bits) & half_mask, r = (uint32_t)v & half_mask;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            uint32_t nl = r, nr = l ^ round_fn(r, i);
-            l = nl;
-            r = nr;
-        }
-        return ((uint64_t)l << half_bits) | r;
-    }
-    __host__ __device__ inline uint64_t operator()(uint64_t t) const {
-        uint64_t v = once(t);
-        while (v >= d) v = once(v);   // cycle walking stays inside [0, d)
-        return v;
-    }
-};
 
 // ------------------------------------------------------------------------------------------
 // Wave helpers

@@ -11,12 +11,15 @@
 //         fallback : rows whose list overflowed, came up short (sample unlucky), or whose K-th
 //                    magnitude is tied ambiguously are redone exactly on the full row
 //                    (3 radix passes + tie prefix + exact filter, ties -> lowest index first)
-//   RandK lists    : per row the K indices (numpy stream, or the device Feistel sampler) are
-//                    bucketed by chunk in two coalesced levels — superchunks in one workgroup
-//                    per row (LDS counts + multi-split), then chunks inside each superchunk (LDS
-//                    counting sort) with the gather of (D/K) * x[j] in ascending order
-//                    (k_randk_coarse / k_randk_fine); a one-level global-atomic path is kept
-//                    behind FLC_RANDK_GLOBAL for A/B runs
+//   RandK device   : the device sampler (randk_tree.hpp) is generated chunk by chunk: per row the
+//                    chunk counts (k_randk_counts, a hypergeometric tree), then one wave per chunk
+//                    regenerates every row's members of its chunk, gathers (D/K) * x[j] and folds
+//                    them in row order (k_randk_fold) — no index lists in memory; the only HBM
+//                    traffic is the gathered 128-B lines and the [D] result
+//   RandK compat   : the K numpy-stream indices of each row are bucketed by chunk in two coalesced
+//                    levels — superchunks in one workgroup per row (LDS counts + multi-split),
+//                    then chunks inside each superchunk (LDS counting sort) with the gather of
+//                    (D/K) * x[j] in ascending order (k_randk_coarse / k_randk_fine)
 //   accumulate     : one wave owns one chunk (or 1/2, 1/4 of it when the rows are short) as an
 //                    fp32 LDS tile and folds the rows' admitted
 //                    entries in row order -> (sum_i w_i C_i(x_i)) / w_total, bit-identical to the
@@ -27,6 +30,7 @@
 #include <stdlib.h>
 
 #include "chunks.hpp"
+#include "randk_tree.hpp"
 
 namespace flc {
 
@@ -717,55 +721,10 @@ __global__ __launch_bounds__(256) void k_tie_scan(int64_t n, int64_t d, SelWs ws
 }
 
 // ------------------------------------------------------------------------------------------
-// RandK lists
+// RandK compat lists (indices given: the reference's numpy-stream draws)
 // ------------------------------------------------------------------------------------------
-__device__ inline int64_t randk_index(const flc_pattern& pat, const Feistel& fe, int64_t row, int64_t t,
-                                      int64_t ldi) {
-    return pat.d_randk_idx ? pat.d_randk_idx[row * ldi + t] : (int64_t)fe((uint64_t)t);
-}
-
-__global__ __launch_bounds__(256) void k_randk_count(int64_t n, int64_t d, int64_t K, flc_pattern pat,
-                                                     int64_t ldi, uint64_t seed, SelWs ws) {
-    const int64_t row = blockIdx.y;
-    Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
-    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
-        int64_t j = randk_index(pat, fe, row, t, ldi);
-        atomicAdd(&ws.cursor[(j >> CHUNK_SHIFT) * n + row], 1u);
-    }
-}
-
-__global__ __launch_bounds__(64) void k_randk_scan(int64_t n, int64_t d, SelWs ws) {
-    const int64_t C = nchunks(d);
-    const int64_t row = blockIdx.x;
-    if (threadIdx.x != 0 || row >= n) return;
-    uint32_t run = 0;
-    for (int64_t c = 0; c < C; ++c) {
-        uint32_t v = ws.cursor[c * n + row];
-        ws.tab[c * n + row] = make_uint2(run, v);
-        ws.cursor[c * n + row] = 0;
-        run += v;
-    }
-    ws.thr[row] = 0;
-    ws.flags[row] = F_EXACT;      // the list holds exactly the kept entries: k_chunk_accum admits all
-    ws.rowcnt[(row) * RCS] = run;
-}
-
-// bucket the row's K indices by chunk (list order inside a chunk is free: the columns are distinct)
-__global__ __launch_bounds__(256) void k_randk_scatter(int64_t n, int64_t d, int64_t K, flc_pattern pat,
-                                                       int64_t ldi, uint64_t seed, SelWs ws) {
-    const int64_t row = blockIdx.y;
-    Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
-    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
-        const int64_t j = randk_index(pat, fe, row, t, ldi);
-        const int64_t slot = (j >> CHUNK_SHIFT) * n + row;
-        const uint32_t pos = ws.tab[slot].x + atomicAdd(&ws.cursor[slot], 1u);
-        ws.ent_idx[row * ws.cap + pos] = (uint32_t)j;
-    }
-}
-
-// Chunk-bucketed RandK lists in two coalesced levels (the global path above evaluates the
-// permutation twice and pays two contended global atomics and a random 4-B write per index).
-//   k_randk_coarse (one workgroup per row): j = perm(t) once, parked in the row's ent_val region;
+// Chunk-bucketed RandK lists in two coalesced levels.
+//   k_randk_coarse (one workgroup per row): the row's K indices copied once into the row's ent_val region;
 //     LDS counts per superchunk (SB buckets of SPC chunks), LDS scan, then each index appended to
 //     its superchunk's segment of ent_idx: SB write frontiers per row, which stay in L2.
 //   k_randk_fine (one workgroup per (superchunk, row)): counting sort of the segment by chunk with
@@ -777,39 +736,16 @@ constexpr int RK_TILE = 8192;                // indices per LDS multi-split tile
 
 __host__ __device__ inline int64_t rk_spc(int64_t C) { return (C + RK_SB - 1) / RK_SB; }   // chunks per superchunk
 
-// Each lane walks its own sequence t = tid, tid + RK_T, ...: one Feistel round-set per loop trip for
-// every lane, an index emitted whenever the cycle walk lands inside [0, d).  (A plain
-// `while (v >= d)` per index idles the wave on its slowest lane: ~10 trips instead of ~2.7.)
 template <class Emit>
-__device__ inline void randk_walk(const flc_pattern& pat, const Feistel& fe, int64_t row, int64_t K, int64_t ldi,
-                                  int tid, Emit emit) {
-    if (pat.d_randk_idx) {
-        for (int64_t t = tid; t < K; t += RK_T) emit(t, (uint32_t)pat.d_randk_idx[row * ldi + t]);
-        return;
-    }
-    int64_t t = tid;
-    bool live = t < K;
-    uint64_t x = (uint64_t)t;
-    while (__ballot(live) != 0ull) {
-        const uint64_t v = fe.once(x);
-        if (live) {
-            if (v < fe.d) {
-                emit(t, (uint32_t)v);
-                t += RK_T;
-                live = t < K;
-                x = (uint64_t)t;
-            } else {
-                x = v;
-            }
-        }
-    }
+__device__ inline void randk_walk(const flc_pattern& pat, int64_t row, int64_t K, int64_t ldi, int tid, Emit emit) {
+    for (int64_t t = tid; t < K; t += RK_T) emit(t, (uint32_t)pat.d_randk_idx[row * ldi + t]);
 }
 
 // FINAL (one chunk per superchunk, C <= RK_SB): the superchunks are the chunks, so this kernel also
 // writes the (offset, count) table and gathers the values; k_randk_fine is skipped.
 template <bool FINAL>
 __global__ __launch_bounds__(RK_T) void k_randk_coarse(RowSrc rows, int64_t n, int64_t d, int64_t K, flc_pattern pat,
-                                                       int64_t ldi, uint64_t seed, float scale, SelWs ws) {
+                                                       int64_t ldi, float scale, SelWs ws) {
     __shared__ uint32_t cnt[RK_SB], tcnt[RK_SB], toff[RK_SB], gbase[RK_SB];
     __shared__ uint32_t tile[RK_TILE];
     const int64_t row = blockIdx.x;
@@ -817,9 +753,8 @@ __global__ __launch_bounds__(RK_T) void k_randk_coarse(RowSrc rows, int64_t n, i
     const int tid = threadIdx.x;
     if (tid < RK_SB) cnt[tid] = 0;
     __syncthreads();
-    const Feistel fe(client_key(seed, pat.client0 + row), (uint64_t)d);
     uint32_t* jbuf = reinterpret_cast<uint32_t*>(ws.ent_val + row * ws.cap);
-    randk_walk(pat, fe, row, K, ldi, tid, [&](int64_t t, uint32_t j) {
+    randk_walk(pat, row, K, ldi, tid, [&](int64_t t, uint32_t j) {
         jbuf[t] = j;
         atomicAdd(&cnt[(j >> CHUNK_SHIFT) / spc], 1u);
     });
@@ -1003,17 +938,6 @@ __global__ __launch_bounds__(RK_FTHR) void k_randk_fine(RowSrc rows, int64_t n, 
     }
     __syncthreads();                                        // block-scope visibility of the idx writes
     for (uint32_t t = s0 + tid; t < s1; t += RK_FTHR) val[t] = scale * r[idx[t]];
-}
-
-// gather (D/K) * x[S] in fp32 in list order: chunk by chunk, so a wave's 64 reads fall in one or two
-// 16 KB windows of the row (HBM page locality) instead of the permutation's random order
-__global__ __launch_bounds__(256) void k_randk_gather(RowSrc rows, int64_t K, float scale, SelWs ws) {
-    const int64_t row = blockIdx.y;
-    const float* r = rows.row(row);
-    const uint32_t* idx = ws.ent_idx + row * ws.cap;
-    float* val = ws.ent_val + row * ws.cap;
-    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256)
-        val[t] = scale * r[idx[t]];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1223,6 +1147,252 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// RandK device mode (randk_tree.hpp): no index lists.
+//   k_randk_counts : one workgroup per row walks the hypergeometric tree level by level (ping-pong
+//                    level arrays in the workspace) -> cnt[c][row] = the row's members in chunk c,
+//                    and the row's client key
+//   k_randk_fold   : one wave per chunk (or 1/2, 1/4 of its columns when the rows are short) folds
+//                    the rows in order into an fp32 LDS tile: row q's members of the chunk are the
+//                    first cnt[c][q] images of the chunk permutation (lane t -> offset P(t)), their
+//                    values (D/K) * x_q[j] gathered with range-checked buffer loads (AP rows in
+//                    flight), added as w_q * v — the sequential fold of the dense compressVector
+//                    outputs, bit for bit (a row's members are distinct)
+// ------------------------------------------------------------------------------------------
+struct RkdWs {
+    uint32_t* cnt;     // [C][N]
+    uint64_t* ckey;    // [N]
+    uint32_t* lev;     // [N][2^(L+1)] tree levels (heap layout)
+    int64_t lstride;   // 2^L
+};
+
+__global__ __launch_bounds__(256) void k_randk_counts(int64_t n, int64_t d, int64_t K, uint64_t seed, int64_t client0,
+                                                      RkdWs ws) {
+    const int64_t row = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint64_t ck = client_key(seed, client0 + row);
+    const int64_t C = nchunks(d);
+    const int L = rktree::tree_depth(C);
+    const uint64_t tk = rktree::tree_key(ck);
+    // heap layout: level l at [2^l, 2^(l+1)) — every word is written once and read only after the
+    // barrier that follows its write (no line of it can sit stale in the CU's L1)
+    uint32_t* H = ws.lev + row * 2 * ws.lstride;
+    if (tid == 0) {
+        ws.ckey[row] = ck;
+        H[1] = (uint32_t)K;
+    }
+    __syncthreads();
+    for (int l = 0; l < L; ++l) {
+        const uint32_t* A = H + ((int64_t)1 << l);
+        uint32_t* B = H + ((int64_t)2 << l);
+        for (int64_t i = tid; i < ((int64_t)1 << l); i += 256) {
+            const int64_t m = A[i];
+            const int64_t x = rktree::node_split(tk, C, d, l, i, m);
+            B[2 * i] = (uint32_t)x;
+            B[2 * i + 1] = (uint32_t)(m - x);
+        }
+        __syncthreads();                                 // block-scope visibility of the level
+    }
+    const uint32_t* A = H + ((int64_t)1 << L);
+    for (int64_t i = tid; i < ((int64_t)1 << L); i += 256) {
+        const int64_t a = rktree::node_lo(C, L, i);
+        if (rktree::node_lo(C, L, i + 1) - a == 1) ws.cnt[a * n + row] = A[i];
+    }
+}
+
+__device__ inline uint64_t join64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | (uint64_t)lo; }
+
+struct RkMeta {            // lane = row of a 64-row batch
+    uint32_t m;            // members of this chunk
+    uint32_t klo, khi;     // client key
+    uint32_t plo, phi;     // row pointer
+    float w;
+};
+
+__device__ inline RkMeta rk_meta(RowSrc rows, const uint32_t* cnt, const uint64_t* ckey, const float* w, int64_t c,
+                                 int64_t n, int64_t r, uint32_t clen) {
+    RkMeta m{0u, 0u, 0u, 0u, 0u, 1.f};
+    if (r < n) {
+        m.m = min(cnt[c * n + r], clen);                 // <= clen by construction; never index past it
+        const uint64_t k = ckey[r];
+        m.klo = (uint32_t)k;
+        m.khi = (uint32_t)(k >> 32);
+        const uintptr_t p = (uintptr_t)rows.row(r);
+        m.plo = (uint32_t)p;
+        m.phi = (uint32_t)((uint64_t)p >> 32);
+        if (w) m.w = w[r];
+    }
+    return m;
+}
+
+// -0 columns after the fold (every kept term was -0, or no row kept the column): the reference's
+// sum is -0 only if every row's term is -0, and a row that did not keep the column adds w * (+0)
+// (resolve_neg_zero above, the same rule).  Walk the rows with a positive-signed weight, regenerate
+// their members of this part, and turn +0 every -0 column some such row does not keep; stops as
+// soon as no candidate is left (normally after the first row).
+template <int TS>
+__device__ void rk_resolve_neg_zero(float* tl, uint32_t* rm, const uint32_t* cnt, const uint64_t* ckey, int64_t c,
+                                    int64_t n, uint32_t pbase, uint32_t clen, int64_t len, const float* w, int lane) {
+    constexpr int NW = TS / 32;
+    constexpr int WL = (NW + 63) / 64;
+    bool any = false;
+    for (int k = 0; k < TS / 64; ++k) {
+        const int64_t i = (int64_t)k * 64 + lane;
+        const uint64_t b = __ballot(i < len && __float_as_uint(tl[i]) == 0x80000000u);
+        if (lane == 0) { rm[2 * k] = (uint32_t)b; rm[2 * k + 1] = (uint32_t)(b >> 32); }
+        any |= b != 0ull;
+    }
+    if (!any) return;
+    uint32_t z0[WL], zc[WL];
+#pragma unroll
+    for (int j = 0; j < WL; ++j) {
+        const int k = lane + 64 * j;
+        z0[j] = k < NW ? rm[k] : 0u;
+        zc[j] = z0[j];
+    }
+    for (int64_t r = 0; r < n; ++r) {
+        if (w && (__float_as_uint(w[r]) >> 31)) continue;
+#pragma unroll
+        for (int j = 0; j < WL; ++j) if (lane + 64 * j < NW) rm[lane + 64 * j] = 0u;
+        const uint32_t m = min(cnt[c * n + r], clen);
+        const rktree::ChunkPerm P(ckey[r], c, clen);
+        for (uint32_t t = (uint32_t)lane; t < m; t += 64) {
+            const uint32_t loc = P(t) - pbase;
+            if (loc < (uint32_t)TS) atomicOr(&rm[loc >> 5], 1u << (loc & 31));
+        }
+        bool left = false;
+#pragma unroll
+        for (int j = 0; j < WL; ++j) {
+            if (lane + 64 * j < NW) zc[j] &= rm[lane + 64 * j];
+            left |= zc[j] != 0u;
+        }
+        if (__ballot(left) == 0ull) break;
+    }
+#pragma unroll
+    for (int j = 0; j < WL; ++j) {
+        uint32_t dead = z0[j] & ~zc[j];
+        while (dead) {
+            const int b = __builtin_ctz(dead);
+            dead &= dead - 1u;
+            tl[(lane + 64 * j) * 32 + b] = 0.f;
+        }
+    }
+}
+
+template <int TS>
+__global__ __launch_bounds__(256) void k_randk_fold(RowSrc rows, int64_t n, int64_t d, const uint32_t* __restrict__ cnt,
+                                                    const uint64_t* __restrict__ ckey, float scale,
+                                                    const float* __restrict__ w, float wt, float* __restrict__ out) {
+    constexpr int PARTS = CHUNK / TS;
+    constexpr uint32_t NOCOL = 0xFFFFu;                    // past the chunk: the buffer load returns 0
+    __shared__ __attribute__((aligned(16))) float tile[4][TS];
+    __shared__ uint32_t zmask[4][TS / 32];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t C = nchunks(d);
+    float* tl = tile[wv];
+    const int64_t nb = (n + 63) / 64;
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < C * PARTS; t += (int64_t)gridDim.x * 4) {
+        const int64_t c = t / PARTS;
+        const uint32_t pbase = (uint32_t)((t % PARTS) * TS);
+        const int64_t cbase = c * CHUNK;
+        const uint32_t clen = (uint32_t)min((int64_t)CHUNK, d - cbase);
+        for (int i = lane; i < TS; i += 64) tl[i] = -0.f;     // the additive identity
+        uint32_t ro[AP];                                      // ring: part-local column (>= TS: none)
+        float rv[AP];                                         //       gathered x
+        // row q of the current batch: its members' columns for this lane, one gather in flight
+        auto fetch = [&](const RkMeta& mt, int q, int slot) {
+            const uint32_t m = __builtin_amdgcn_readlane(mt.m, q);
+            // readlane returns int: widen through uint32_t (a sign-extended low word would set the high one)
+            const uint64_t k = join64((uint32_t)__builtin_amdgcn_readlane(mt.khi, q), (uint32_t)__builtin_amdgcn_readlane(mt.klo, q));
+            const float* rp = (const float*)join64((uint32_t)__builtin_amdgcn_readlane(mt.phi, q),
+                                                   (uint32_t)__builtin_amdgcn_readlane(mt.plo, q));
+            const rktree::ChunkPerm P(k, c, clen);
+            uint32_t col = (uint32_t)lane < m ? P((uint32_t)lane) : NOCOL;
+            if (PARTS > 1 && col - pbase >= (uint32_t)TS) col = NOCOL;   // another wave's part: no gather
+            const auto rs = chunk_rsrc(rp ? rp : rows.base, cbase, d);
+            ro[slot] = col - pbase;
+            rv[slot] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(col * 4u), 0, 0));
+        };
+        auto fold = [&](int slot, float wi) {
+            const uint32_t loc = ro[slot];
+            if (loc < (uint32_t)TS) tl[loc] = tl[loc] + wi * (scale * rv[slot]);
+        };
+        RkMeta cur = rk_meta(rows, cnt, ckey, w, c, n, lane, clen), nxt;
+#pragma unroll
+        for (int q = 0; q < AP; ++q) fetch(cur, q, q);
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t i0 = b * 64;
+            nxt = rk_meta(rows, cnt, ckey, w, c, n, i0 + 64 + lane, clen);
+            if (__builtin_expect(__ballot(cur.m > 64u) == 0ull, 1)) {
+#pragma unroll
+                for (int q = 0; q < 64; ++q) {
+                    const int slot = q % AP;
+                    fold(slot, __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.w), q)));
+                    if (q + AP < 64) fetch(cur, q + AP, slot);
+                    else fetch(nxt, q + AP - 64, slot);
+                }
+            } else {
+                // a row with more than 64 members here: the same walk with its tail folded in place
+                for (int q = 0; q < 64; ++q) {
+                    const int slot = q % AP;
+                    const float wi = __shfl(cur.w, q, WAVE);
+                    uint32_t lo = NOCOL;
+                    float vv = 0.f;
+#pragma unroll
+                    for (int z = 0; z < AP; ++z)
+                        if (z == slot) { lo = ro[z]; vv = rv[z]; }
+                    if (lo < (uint32_t)TS) tl[lo] = tl[lo] + wi * (scale * vv);
+                    const uint32_t m = __shfl(cur.m, q, WAVE);
+                    if (m > 64u) {
+                        const int64_t row = i0 + q;
+                        const rktree::ChunkPerm P(ckey[row], c, clen);
+                        const float* rp = rows.row(row);
+                        for (uint32_t e = 64u + lane; e < m; e += 64) {
+                            const uint32_t col = P(e), l2 = col - pbase;
+                            if (l2 < (uint32_t)TS) tl[l2] = tl[l2] + wi * (scale * rp[cbase + col]);
+                        }
+                    }
+                    // refill the slot (same contract as the straight-line path)
+                    const RkMeta& mt = (q + AP < 64) ? cur : nxt;
+                    const int qq = (q + AP) & 63;
+                    const uint32_t mn = __shfl(mt.m, qq, WAVE);
+                    const uint64_t kn = join64((uint32_t)__shfl(mt.khi, qq, WAVE), (uint32_t)__shfl(mt.klo, qq, WAVE));
+                    const float* rpn = (const float*)join64((uint32_t)__shfl(mt.phi, qq, WAVE), (uint32_t)__shfl(mt.plo, qq, WAVE));
+                    const rktree::ChunkPerm Pn(kn, c, clen);
+                    const uint32_t col = (uint32_t)lane < mn ? Pn((uint32_t)lane) : NOCOL;
+                    const float xv = col < clen ? rpn[cbase + col] : 0.f;
+#pragma unroll
+                    for (int z = 0; z < AP; ++z)
+                        if (z == slot) { ro[z] = col - pbase; rv[z] = xv; }
+                }
+            }
+            cur = nxt;
+        }
+        const int64_t len = min((int64_t)TS, (int64_t)clen - (int64_t)pbase);
+        rk_resolve_neg_zero<TS>(tl, zmask[wv], cnt, ckey, c, n, pbase, clen, len, w, lane);
+        for (int64_t i = lane; i < len; i += 64) out[cbase + pbase + i] = tl[i] / wt;
+    }
+}
+
+// Single row (compressVector): out = 0, then each wave writes the members of its chunks
+__global__ __launch_bounds__(256) void k_randk_scatter_dev(const float* __restrict__ x, int64_t d, const uint32_t* cnt,
+                                                           const uint64_t* ckey, float scale, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t C = nchunks(d);
+    const uint64_t k = ckey[0];
+    for (int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64; c < C; c += (int64_t)gridDim.x * 4) {
+        const int64_t cbase = c * CHUNK;
+        const uint32_t clen = (uint32_t)min((int64_t)CHUNK, d - cbase);
+        const rktree::ChunkPerm P(k, c, clen);
+        const uint32_t m = min(cnt[c], clen);
+        for (uint32_t t = (uint32_t)lane; t < m; t += 64) {
+            const int64_t j = cbase + P(t);
+            out[j] = scale * x[j];
+        }
+    }
+}
+
 // Single-row dense output (compressVector: out = zeros; out[admitted] = x, stored not added, so a
 // selected -0.0 stays -0.0 like torch's out[ind] = x[ind]): after a memset, the row's list
 // (entries [0, rowcnt), distinct indices) is scattered with the fold's admission rule — no per-chunk
@@ -1282,9 +1452,13 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     return s;
 }
 
+size_t randk_device_workspace(int64_t n, int64_t d);
+
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     size_t b = 0;
     carve_sel(nullptr, prm->codec, n, d, prm->k, &b);
+    // RandK: the pattern (compat lists or device draws) is not known at the size query
+    if (prm->codec == FLC_RANDK) b = std::max(b, randk_device_workspace(n, d));
     return b;
 }
 
@@ -1319,6 +1493,82 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream
     hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
 }
 
+static RkdWs carve_rkd(void* base, int64_t n, int64_t d, size_t* bytes) {
+    Carver cv(base);
+    const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
+    RkdWs s;
+    s.lstride = (int64_t)1 << rktree::tree_depth(C);
+    s.cnt = cv.take<uint32_t>((size_t)C * nn);
+    s.ckey = cv.take<uint64_t>((size_t)nn);
+    s.lev = cv.take<uint32_t>((size_t)nn * 2 * s.lstride);
+    if (bytes) *bytes = cv.bytes();
+    return s;
+}
+
+size_t randk_device_workspace(int64_t n, int64_t d) {
+    size_t b = 0;
+    carve_rkd(nullptr, n, d, &b);
+    return b;
+}
+
+static int randk_counts(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d, RkdWs ws,
+                        hipStream_t st) {
+    ProfScope _ps("k_randk_counts", st);
+    hipLaunchKernelGGL(k_randk_counts, dim3((unsigned)n), dim3(256), 0, st, n, d, prm->k, prm->seed,
+                       pat ? pat->client0 : (int64_t)0, ws);
+    FLC_CHECK_LAUNCH("k_randk_counts");
+    return FLC_OK;
+}
+
+// the device sampler's chunk counts of n clients (flc_device_randk_counts: the sampler's test hook)
+int randk_device_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, int64_t k, uint32_t* cnt, void* wsp,
+                        size_t ws_bytes, hipStream_t st) {
+    if (ws_bytes < randk_device_workspace(n, d)) { set_error("randk counts: workspace too small"); return FLC_ERR_WORKSPACE; }
+    RkdWs ws = carve_rkd(wsp, n, d, nullptr);
+    flc_codec_params prm{};
+    prm.codec = FLC_RANDK;
+    prm.k = k;
+    prm.seed = seed;
+    flc_pattern pat{};
+    pat.client0 = client0;
+    if (int rc = randk_counts(&prm, &pat, n, d, ws, st)) return rc;
+    FLC_CHECK_HIP(hipMemcpyAsync(cnt, ws.cnt, (size_t)host_chunks(d) * n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    return FLC_OK;
+}
+
+// device-RNG RandK encode + reduce: counts, then the list-free chunk fold
+int randk_device_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d,
+                     const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
+    if (ws_bytes < randk_device_workspace(n, d)) { set_error("randk: workspace too small"); return FLC_ERR_WORKSPACE; }
+    RkdWs ws = carve_rkd(wsp, n, d, nullptr);
+    if (int rc = randk_counts(prm, pat, n, d, ws, st)) return rc;
+    const int64_t C = host_chunks(d);
+    // few chunks (short rows: C2's D = 1 M has 245): each chunk's columns over up to 16 waves, so
+    // the row-serial walk runs on ~8 K waves (each wave still regenerates all of a row's members of
+    // the chunk, but gathers only those in its part)
+    int parts = 1;
+    while (parts < 16 && parts * C < 8192) parts *= 2;
+    const int ab = grid_stride_blocks((parts * C + 3) / 4, 16384);
+    ProfScope _ps("k_randk_fold", st);
+    if (parts == 16)
+        hipLaunchKernelGGL((k_randk_fold<CHUNK / 16>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
+                           prm->randk_scale, w, wt, out);
+    else if (parts == 8)
+        hipLaunchKernelGGL((k_randk_fold<CHUNK / 8>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
+                           prm->randk_scale, w, wt, out);
+    else if (parts == 4)
+        hipLaunchKernelGGL((k_randk_fold<CHUNK / 4>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
+                           prm->randk_scale, w, wt, out);
+    else if (parts == 2)
+        hipLaunchKernelGGL((k_randk_fold<CHUNK / 2>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
+                           prm->randk_scale, w, wt, out);
+    else
+        hipLaunchKernelGGL((k_randk_fold<CHUNK>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
+                           prm->randk_scale, w, wt, out);
+    FLC_CHECK_LAUNCH("k_randk_fold");
+    return FLC_OK;
+}
+
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
     const int codec = prm->codec;
@@ -1327,43 +1577,29 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (n == 0) { FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st)); return FLC_OK; }
     if (K < 1 || K > d) { set_error("K=%lld outside [1, D=%lld]", (long long)K, (long long)d); return FLC_ERR_ARG; }
     if (d >= (int64_t)0xFFFFFFFF) { set_error("D too large for 32-bit entry indices"); return FLC_ERR_ARG; }
+    if (codec == FLC_RANDK && !(pat && pat->d_randk_idx))
+        return randk_device_run(prm, pat, rows, n, d, w, wt, out, wsp, ws_bytes, st);
     size_t need = 0;
     carve_sel(nullptr, codec, n, d, K, &need);
     if (ws_bytes < need) { set_error("select: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
     SelWs ws = carve_sel(wsp, codec, n, d, K, nullptr);
     const int64_t C = host_chunks(d);
     if (codec == FLC_RANDK) {
-        const int64_t ldi = (pat && pat->idx_ld) ? pat->idx_ld : K;
-        flc_pattern p = pat ? *pat : flc_pattern{};
-        dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>((K + 255) / 256, 64)), (unsigned)n);
-        if (!tuning_env("FLC_RANDK_GLOBAL")) {
-            const int64_t spc = rk_spc(C), sb = (C + spc - 1) / spc;
-            { ProfScope _ps("k_randk_coarse", st);
-            if (spc == 1)
-                hipLaunchKernelGGL(k_randk_coarse<true>, dim3((unsigned)n), dim3(RK_T), 0, st, rows, n, d, K, p, ldi,
-                                   prm->seed, prm->randk_scale, ws);
-            else
-                hipLaunchKernelGGL(k_randk_coarse<false>, dim3((unsigned)n), dim3(RK_T), 0, st, rows, n, d, K, p, ldi,
-                                   prm->seed, prm->randk_scale, ws); }
-            FLC_CHECK_LAUNCH("k_randk_coarse");
-            if (spc > 1) {
-                ProfScope _ps("k_randk_fine", st);
-                hipLaunchKernelGGL(k_randk_fine, dim3((unsigned)sb, (unsigned)n), dim3(RK_FTHR), (size_t)spc * sizeof(uint32_t),
-                                   st, rows, n, d, K, prm->randk_scale, ws);
-                FLC_CHECK_LAUNCH("k_randk_fine");
-            }
-        } else {
-            FLC_CHECK_HIP(hipMemsetAsync(ws.cursor, 0, (size_t)C * n * sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_randk_count, g, dim3(256), 0, st, n, d, K, p, ldi, prm->seed, ws);
-            FLC_CHECK_LAUNCH("k_randk_count");
-            hipLaunchKernelGGL(k_randk_scan, dim3((unsigned)n), dim3(64), 0, st, n, d, ws);
-            FLC_CHECK_LAUNCH("k_randk_scan");
-            { ProfScope _ps("k_randk_scatter", st);
-            hipLaunchKernelGGL(k_randk_scatter, g, dim3(256), 0, st, n, d, K, p, ldi, prm->seed, ws); }
-            FLC_CHECK_LAUNCH("k_randk_scatter");
-            { ProfScope _ps("k_randk_gather", st);
-            hipLaunchKernelGGL(k_randk_gather, g, dim3(256), 0, st, rows, K, prm->randk_scale, ws); }
-            FLC_CHECK_LAUNCH("k_randk_gather");
+        const int64_t ldi = pat->idx_ld ? pat->idx_ld : K;
+        const int64_t spc = rk_spc(C), sb = (C + spc - 1) / spc;
+        { ProfScope _ps("k_randk_coarse", st);
+        if (spc == 1)
+            hipLaunchKernelGGL(k_randk_coarse<true>, dim3((unsigned)n), dim3(RK_T), 0, st, rows, n, d, K, *pat, ldi,
+                               prm->randk_scale, ws);
+        else
+            hipLaunchKernelGGL(k_randk_coarse<false>, dim3((unsigned)n), dim3(RK_T), 0, st, rows, n, d, K, *pat, ldi,
+                               prm->randk_scale, ws); }
+        FLC_CHECK_LAUNCH("k_randk_coarse");
+        if (spc > 1) {
+            ProfScope _ps("k_randk_fine", st);
+            hipLaunchKernelGGL(k_randk_fine, dim3((unsigned)sb, (unsigned)n), dim3(RK_FTHR), (size_t)spc * sizeof(uint32_t),
+                               st, rows, n, d, K, prm->randk_scale, ws);
+            FLC_CHECK_LAUNCH("k_randk_fine");
         }
     } else {  // TOPK
         FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
@@ -1512,24 +1748,31 @@ int sel_unpack_reduce(const flc_codec_params* prm, const void* base, int64_t ld_
 }
 
 // Dense single-vector RandK: out = 0; out[S] = scale * x[S]  (compressors.py:242-243)
-__global__ __launch_bounds__(256) void k_randk_dense(const float* __restrict__ x, int64_t d, int64_t K, flc_pattern pat,
-                                                     uint64_t seed, float scale, float* __restrict__ out) {
-    Feistel fe(client_key(seed, pat.client0), (uint64_t)d);
+__global__ __launch_bounds__(256) void k_randk_dense(const float* __restrict__ x, int64_t K, const int64_t* __restrict__ idx,
+                                                     float scale, float* __restrict__ out) {
     for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < K; t += (int64_t)gridDim.x * 256) {
-        const int64_t j = randk_index(pat, fe, 0, t, K);
+        const int64_t j = idx[t];
         out[j] = scale * x[j];
     }
 }
 
 int randk_dense(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, float* out,
-                hipStream_t st) {
+                void* wsp, size_t ws_bytes, hipStream_t st) {
     if (d == 0) return FLC_OK;
     if (prm->k < 1 || prm->k > d) { set_error("randk: K outside [1, D]"); return FLC_ERR_ARG; }
     FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
-    flc_pattern p = pat ? *pat : flc_pattern{};
-    int g = (int)std::max<int64_t>(1, std::min<int64_t>((prm->k + 255) / 256, 1024));
-    hipLaunchKernelGGL(k_randk_dense, dim3(g), dim3(256), 0, st, x, d, prm->k, p, prm->seed, prm->randk_scale, out);
-    FLC_CHECK_LAUNCH("k_randk_dense");
+    if (pat && pat->d_randk_idx) {
+        int g = (int)std::max<int64_t>(1, std::min<int64_t>((prm->k + 255) / 256, 1024));
+        hipLaunchKernelGGL(k_randk_dense, dim3(g), dim3(256), 0, st, x, prm->k, pat->d_randk_idx, prm->randk_scale, out);
+        FLC_CHECK_LAUNCH("k_randk_dense");
+        return FLC_OK;
+    }
+    if (ws_bytes < randk_device_workspace(1, d)) { set_error("randk: workspace too small"); return FLC_ERR_WORKSPACE; }
+    RkdWs ws = carve_rkd(wsp, 1, d, nullptr);
+    if (int rc = randk_counts(prm, pat, 1, d, ws, st)) return rc;
+    const int g = grid_stride_blocks((host_chunks(d) + 3) / 4, 4096);
+    hipLaunchKernelGGL(k_randk_scatter_dev, dim3(g), dim3(256), 0, st, x, d, ws.cnt, ws.ckey, prm->randk_scale, out);
+    FLC_CHECK_LAUNCH("k_randk_scatter_dev");
     return FLC_OK;
 }
 

@@ -48,7 +48,7 @@ static bool shift_elementwise(int codec) { return codec != FLC_RANDK && codec !=
 static size_t inner_workspace(const flc_codec_params* prm, int64_t d) {
     if (prm->codec == FLC_TOPK) return sel_workspace(prm, 1, d);
     if (prm->codec == FLC_RANK_K) return rk_workspace(prm, 1, d, false);
-    return 0;   // RandK's single-row encode needs none
+    return randk_device_workspace(1, d);   // RandK: the device draws' chunk counts
 }
 
 size_t shift_workspace(const flc_codec_params* prm, int64_t d) {
@@ -85,7 +85,7 @@ int shift_run(const flc_codec_params* prm, const flc_pattern* pat, const float* 
     RowSrc r{diff, d, nullptr};
     if (prm->codec == FLC_RANDK) {
         if (!(pat && pat->d_randk_idx) && prm->k > d) { set_error("randk: K > D"); return FLC_ERR_ARG; }
-        rc = randk_dense(prm, pat, diff, d, e, st);
+        rc = randk_dense(prm, pat, diff, d, e, iws, inner, st);
     } else if (prm->codec == FLC_TOPK) {
         rc = sel_run(prm, pat, r, true, 1, d, /*assign=*/true, nullptr, 1.f, e, iws, inner, st);
     } else {

@@ -252,6 +252,13 @@ int flc_mt_randint31(uint32_t* h_key, int32_t* h_pos, int64_t count, int64_t* h_
  * kernels draw for (seed, client, element). */
 double flc_device_uniform(uint64_t seed, int64_t client, int64_t j);
 int flc_device_randk_indices(uint64_t seed, int64_t client, int64_t d, int64_t k, int64_t* h_out);
+/* The device sampler's per-chunk member counts of clients client0 .. client0 + n - 1, computed by
+ * the kernel the fused RandK path runs (k_randk_counts), into d_counts[C][n] (C = ceil(d / 4096),
+ * uint32, chunk-major): the GPU-side check of the sampler against its host mirror and the numpy
+ * restatement.  Workspace of flc_device_randk_counts_workspace_size bytes; enqueued on stream. */
+size_t flc_device_randk_counts_workspace_size(int64_t n, int64_t d);
+int flc_device_randk_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, int64_t k, uint32_t* d_counts,
+                            void* d_ws, size_t ws_bytes, void* stream);
 
 /* Self-test of the exact fast fp32 division the dithering kernels use: for each of the n
  * device divisors, every float numerator in [2^-80, 2^80] is divided both ways and the

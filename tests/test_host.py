@@ -131,13 +131,86 @@ def test_compute_without_gpu_fails_loudly():
 
 def test_device_rng_host_mirror():
     lib = _lib.load()
-    for d, k in [(1, 1), (7, 3), (1000, 10), (4097, 4097), (1 << 20, 10486)]:
+    for d, k in [(1, 1), (7, 3), (1000, 10), (4097, 4097), (1 << 20, 10486), (4096 * 5 + 7, 20000)]:
         idx = np.empty(k, dtype=np.int64)
         assert lib.flc_device_randk_indices(42, 3, d, k, idx.ctypes.data) == 0
         assert idx.min() >= 0 and idx.max() < d and np.unique(idx).size == k
     u = np.array([lib.flc_device_uniform(42, 3, j) for j in range(20000)])
     assert u.min() >= 0.0 and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01
     assert math.isclose(np.var(u), 1 / 12, rel_tol=0.03)
+
+
+@pytest.mark.parametrize("seed,client,d,k", [(42, 3, 1, 1), (42, 3, 7, 3), (1, 0, 4096, 4096), (42, 3, 4097, 4097),
+                                             (5, 9, 1_000_000, 10_000), (7, 2, 4096 * 3 + 5, 100),
+                                             (2**63 + 5, 10**9, 10_000_000, 100_000), (3, 4, 65536, 1)])
+def test_device_randk_oracle_restatement(seed, client, d, k):
+    """oracle/devrng.py restates the device RandK sampler (randk_tree.hpp: hypergeometric chunk
+    counts + chunk permutations) in Python floats; it equals the library's host mirror bit for bit."""
+    from oracle import devrng
+    lib = _lib.load()
+    want = np.empty(k, dtype=np.int64)
+    assert lib.flc_device_randk_indices(seed, client, d, k, want.ctypes.data) == 0
+    got = devrng.randk_indices(seed, client, d, k)
+    assert np.array_equal(got, want)
+    assert np.unique(got).size == k and got.min() >= 0 and got.max() < d
+    assert devrng.randk_counts(seed, client, d, k).sum() == k
+
+
+def test_device_randk_hypergeometric_pmf():
+    """The sampler's dhyper (Loader's saddle-point form, deterministic log / exp) against the pmf in
+    40-digit arithmetic (mpmath; scipy's float64 pmf is itself ~1e-8 off at N = 1e8), and the
+    inversion's law against the pmf (chi-square over 20 000 draws)."""
+    import mpmath
+    from scipy import stats
+    from oracle import devrng
+    mpmath.mp.dps = 40
+    lg = mpmath.loggamma
+
+    def pmf(x, N, r, m):
+        b = N - r
+        return float(mpmath.exp(lg(r + 1) - lg(x + 1) - lg(r - x + 1) + lg(b + 1) - lg(m - x + 1) - lg(b - m + x + 1)
+                                - lg(N + 1) + lg(m + 1) + lg(N - m + 1)))
+    for N, r, m in [(8192, 4096, 82), (100_000_000, 50_003_968, 1_000_000), (12293, 8192, 100), (50, 7, 20),
+                    (2**32 - 1, 2**31, 3)]:
+        lo, hi = max(0, m - (N - r)), min(r, m)
+        mode = (m + 1) * (r + 1) // (N + 2)
+        for x in sorted({lo, hi, mode, min(hi, mode + 3), max(lo, mode - 5)}):
+            want = pmf(x, N, r, m)
+            got = devrng.dhyper(x, r, N - r, m)
+            assert math.isclose(got, want, rel_tol=1e-12, abs_tol=1e-300), (N, r, m, x, got, want)
+    N, r, m = 8192, 4096, 82
+    rng = np.random.default_rng(0)
+    xs = np.array([devrng.hyper_draw(N, r, m, float(u)) for u in rng.random(20000)])
+    vals, cnt = np.unique(xs, return_counts=True)
+    exp = stats.hypergeom.pmf(vals, N, r, m) * xs.size
+    keep = exp > 5
+    chi2 = (((cnt - exp) ** 2) / exp)[keep].sum()
+    assert chi2 < stats.chi2.ppf(0.999, keep.sum() - 1)
+
+
+def test_device_randk_is_uniform():
+    """Device RandK sets are uniform K-subsets: every element kept with probability K/D (the
+    unbiasedness RandK's w = D/K - 1 assumes) and chunk counts with the hypergeometric variance."""
+    lib = _lib.load()
+    d, k, clients = 4096 * 6 + 1000, 500, 3000
+    hits = np.zeros(d)
+    counts = []
+    for cl in range(clients):
+        idx = np.empty(k, dtype=np.int64)
+        assert lib.flc_device_randk_indices(77, cl, d, k, idx.ctypes.data) == 0
+        hits[idx] += 1
+        counts.append(np.bincount(idx // 4096, minlength=7))
+    p = k / d
+    # per-element frequency: binomial(clients, p) per element
+    z = (hits - clients * p) / math.sqrt(clients * p * (1 - p))
+    assert abs(z.mean()) < 0.05 and 0.9 < z.std() < 1.1
+    counts = np.array(counts)
+    for c in range(7):
+        size = min(4096, d - c * 4096)
+        q = size / d
+        mean, var = k * q, k * q * (1 - q) * (d - k) / (d - 1)
+        assert abs(counts[:, c].mean() - mean) < 4 * math.sqrt(var / clients)
+        assert 0.85 < counts[:, c].var() / var < 1.15
 
 
 def test_device_rng_oracle_restatement():
