@@ -46,8 +46,8 @@ PEAK_GBS = 8000.0   # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level paramet
 WORKLOADS = {
     "c3": dict(spec="topk:1%", n=1024, d=10_000_000, kernel="k_topk_filter", config=2, n_total=1024,
                others=["k_topk_sample", "k_cand_select", "k_chunk_accum"]),
-    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_fold", config=1, n_total=256,
-               others=["k_randk_counts"]),
+    "c2": dict(spec="randk:1%", n=256, d=1_000_000, kernel="k_randk_gen", config=1, n_total=256,
+               others=["k_randk_counts", "k_chunk_accum"]),
     # sparse QSGD path (dither_sparse.hip): one read of every row in k_ds_filter
     "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3, n_total=4096,
                others=["k_ds_sample", "k_ds_accum"]),
@@ -78,7 +78,9 @@ def algorithmic_bytes(spec, n, d, k, specs=None):
 def kernel_bytes(kernel, n, d, k):
     """Algorithmic bytes one launch of the dominant kernel must move."""
     if kernel == "k_randk_fold":
-        return 4 * n * k + 4 * d    # device RandK: gather K values per row, write the [D] result
+        return 4 * n * k + 4 * d    # device RandK, long rows: gather K values per row, write the [D] result
+    if kernel == "k_randk_gen":
+        return 4 * n * k            # device RandK, short rows: gather K values per row (into the fold's lists)
     if kernel == "k_randk_coarse":
         return 8 * n * k            # compat RandK (one chunk per superchunk): gather K values per row + write them
     if kernel in ("k_ew_accum_vec", "k_reduce_vec"):
@@ -549,11 +551,11 @@ def main():
     kstep_ms = kms / args.steps
     achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
     line_floor = None
-    if wl["kernel"] == "k_randk_fold":
+    if wl["kernel"] in ("k_randk_fold", "k_randk_gen"):
         # sparse 4-B gathers fetch whole 128-B lines (profiles/r02/probe_gather_fetch.txt): the
         # gather's physical floor is the expected number of distinct lines touched, x 128 B
         nr = len(range(specs.index("randk:1%"), n, len(specs))) if mixed else n
-        line_floor = nr * (d / 32.0) * (1.0 - (1.0 - k / d) ** 32) * 128 + 4 * d
+        line_floor = nr * (d / 32.0) * (1.0 - (1.0 - k / d) ** 32) * 128 + (4 * d if wl["kernel"] == "k_randk_fold" else 0)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):

@@ -12,6 +12,7 @@
 //      53-bit uniform keyed by (client key, node id 2^l + i);
 //   2. inside chunk c, the first m_c images of a keyed 12-bit permutation (4-round Feistel on 6 + 6
 //      bits, cycle-walked into a short last chunk): a uniform m_c-subset of the chunk.
+// (Nodes with at most 64 members draw their split member by member with integer arithmetic.)
 // Given exact hypergeometric counts and uniform within-chunk subsets, the union is a uniform K-subset
 // (the law of choice(D, K, replace=False)); exactly K distinct indices, each kept with probability
 // K / D (RandK's unbiasedness, compressors.py:136's w = D/K - 1).
@@ -90,25 +91,13 @@ __host__ __device__ inline double dexp(double x) {
 // ---- Loader's binomial / hypergeometric densities ---------------------------------------------
 // stirlerr(n) = log(n!) - (n + 1/2) log n + n - log sqrt(2 pi), integer n >= 0 (0 -> 0)
 __host__ __device__ inline double stirlerr(double n) {
-    if (n <= 15.0) {
-        switch ((int)n) {
-            case 1: return 0.08106146679532726;
-            case 2: return 0.0413406959554093;
-            case 3: return 0.02767792568499834;
-            case 4: return 0.020790672103765093;
-            case 5: return 0.016644691189821193;
-            case 6: return 0.013876128823070748;
-            case 7: return 0.01189670994589177;
-            case 8: return 0.010411265261972096;
-            case 9: return 0.009255462182712733;
-            case 10: return 0.00833056343336287;
-            case 11: return 0.007573675487951841;
-            case 12: return 0.00694284010720953;
-            case 13: return 0.006408994188004207;
-            case 14: return 0.0059513701127588475;
-            case 15: return 0.005554733551962801;
-            default: return 0.0;
-        }
+    if (n <= 15.0) {                                        // a table read, no branch per value
+        constexpr double T[16] = {0.0, 0.08106146679532726, 0.0413406959554093, 0.02767792568499834,
+                                  0.020790672103765093, 0.016644691189821193, 0.013876128823070748,
+                                  0.01189670994589177, 0.010411265261972096, 0.009255462182712733,
+                                  0.00833056343336287, 0.007573675487951841, 0.00694284010720953,
+                                  0.006408994188004207, 0.0059513701127588475, 0.005554733551962801};
+        return T[(int)n];
     }
     const double S0 = 1.0 / 12.0, S1 = 1.0 / 360.0, S2 = 1.0 / 1260.0, S3 = 1.0 / 1680.0, S4 = 1.0 / 1188.0;
     const double nn = n * n;
@@ -118,16 +107,30 @@ __host__ __device__ inline double stirlerr(double n) {
     return (S0 - (S1 - (S2 - (S3 - S4 / nn) / nn) / nn) / nn) / n;
 }
 
-// deviance term x log(x / np) + np - x, by its series when x ~ np
-__host__ __device__ inline double bd0(double x, double np) {
+// The density code is called out of line (and its loops kept rolled): inlined into the tree walk it
+// grew the counts kernel to ~15 K instructions, past the instruction cache.
+#define RK_COLD __host__ __device__ inline __attribute__((noinline))
+
+// deviance term x log(x / np) + np - x, by its series when x ~ np (|v| < 0.1: <= 17 terms)
+RK_COLD double bd0(double x, double np) {
     if (fabs(x - np) < 0.1 * (x + np)) {
         double v = (x - np) / (x + np);
         double s = (x - np) * v;
         double ej = 2.0 * x * v;
         v = v * v;
-        for (int j = 1; j < 1000; ++j) {
+        // 1 / (2j + 1), j = 1 ..
+        constexpr double R[24] = {0.3333333333333333, 0.2, 0.14285714285714285, 0.1111111111111111,
+                                  0.09090909090909091, 0.07692307692307693, 0.06666666666666667,
+                                  0.058823529411764705, 0.05263157894736842, 0.047619047619047616,
+                                  0.043478260869565216, 0.04, 0.037037037037037035, 0.034482758620689655,
+                                  0.03225806451612903, 0.030303030303030304, 0.02857142857142857,
+                                  0.02702702702702703, 0.02564102564102564, 0.024390243902439025,
+                                  0.023255813953488372, 0.022222222222222223, 0.02127659574468085,
+                                  0.02040816326530612};
+#pragma unroll 1
+        for (int j = 0; j < 24; ++j) {
             ej = ej * v;
-            const double s1 = s + ej / (double)(2 * j + 1);
+            const double s1 = s + ej * R[j];
             if (s1 == s) return s1;
             s = s1;
         }
@@ -138,7 +141,7 @@ __host__ __device__ inline double bd0(double x, double np) {
 
 constexpr double LN_2PI = 1.8378770664093456;
 
-__host__ __device__ inline double dbinom_raw(double x, double n, double p, double q) {
+RK_COLD double dbinom_raw(double x, double n, double p, double q) {
     if (p == 0.0) return x == 0.0 ? 1.0 : 0.0;
     if (q == 0.0) return x == n ? 1.0 : 0.0;
     if (x == 0.0) {
@@ -152,21 +155,31 @@ __host__ __device__ inline double dbinom_raw(double x, double n, double p, doubl
     return dexp(lc - 0.5 * lf);
 }
 
-// P(X = x), X = successes among m draws without replacement from r successes and b failures
-__host__ __device__ inline double dhyper(double x, double r, double b, double m) {
+// P(X = x), X = successes among m draws without replacement from r successes and b failures:
+// Loader's p1 p2 / p3 of three binomial densities (R's dhyper), with the three saddle-point terms
+// combined under one exp and their three log factors under one log when x is interior
+RK_COLD double dhyper(double x, double r, double b, double m) {
     if (x < 0.0 || m < x || r < x || m - x > b) return 0.0;
     if (m == 0.0) return x == 0.0 ? 1.0 : 0.0;
-    const double p = m / (r + b), q = (r + b - m) / (r + b);
-    const double p1 = dbinom_raw(x, r, p, q);
-    const double p2 = dbinom_raw(m - x, b, p, q);
-    const double p3 = dbinom_raw(m, r + b, p, q);
-    return p1 * p2 / p3;
+    const double N = r + b, p = m / N, q = (N - m) / N;
+    const double y = m - x, z = b - y;                      // failures drawn / left
+    if (x == 0.0 || x == r || y == 0.0 || z == 0.0 || m == N) {
+        const double p1 = dbinom_raw(x, r, p, q);
+        const double p2 = dbinom_raw(y, b, p, q);
+        const double p3 = dbinom_raw(m, N, p, q);
+        return p1 * p2 / p3;
+    }
+    const double lc = (stirlerr(r) - stirlerr(x) - stirlerr(r - x) - bd0(x, r * p) - bd0(r - x, r * q)) +
+                      (stirlerr(b) - stirlerr(y) - stirlerr(z) - bd0(y, b * p) - bd0(z, b * q)) -
+                      (stirlerr(N) - stirlerr(m) - stirlerr(N - m) - bd0(m, N * p) - bd0(N - m, N * q));
+    const double lf = LN_2PI + dlog(((x * (r - x)) / r) * ((y * z) / b) * (N / (m * (N - m))));
+    return dexp(lc - 0.5 * lf);
 }
 
 // Inversion of the hypergeometric law from u in [0, 1): the values are visited from the mode
 // outwards (x0, x0 + 1, x0 - 1, x0 + 2, ...), u is reduced by each value's mass, and the value that
 // takes u below 0 is returned — any fixed visiting order inverts the law exactly.
-__host__ __device__ inline int64_t hyper_draw(int64_t N, int64_t r, int64_t m, double u) {
+RK_COLD int64_t hyper_draw(int64_t N, int64_t r, int64_t m, double u) {
     if (m <= 0 || r <= 0) return 0;
     if (r >= N) return m;
     if (m >= N) return r;
@@ -181,26 +194,41 @@ __host__ __device__ inline int64_t hyper_draw(int64_t N, int64_t r, int64_t m, d
     if (u < 0.0) return x0;
     int64_t lo = x0, hi = x0;
     double plo = p0, phi = p0;
+    // Four steps per side at a time: their ratios are independent of the running masses, so the
+    // divisions overlap; the masses are then updated and tested in the one-step order (the values
+    // are those of the step-by-step walk).
     for (;;) {
-        bool moved = false;
-        if (hi < xmax) {        // P(x + 1) / P(x) = (r - x)(m - x) / ((x + 1)(N - r - m + x + 1))
-            const double x = (double)hi;
-            phi = phi * (((rr - x) * (mm - x)) / ((x + 1.0) * (tail + x + 1.0)));
-            ++hi;
-            u = u - phi;
-            if (u < 0.0) return hi;
-            moved = true;
+        double ru[4], rd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // P(x + 1) / P(x) = (r - x)(m - x) / ((x + 1)(N - r - m + x + 1))
+            const double x = (double)(hi + k);
+            ru[k] = ((rr - x) * (mm - x)) / ((x + 1.0) * (tail + x + 1.0));
         }
-        if (lo > xmin) {        // P(x - 1) / P(x) = x (N - r - m + x) / ((r - x + 1)(m - x + 1))
-            const double x = (double)lo;
-            plo = plo * ((x * (tail + x)) / ((rr - x + 1.0) * (mm - x + 1.0)));
-            --lo;
-            u = u - plo;
-            if (u < 0.0) return lo;
-            moved = true;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // P(x - 1) / P(x) = x (N - r - m + x) / ((r - x + 1)(m - x + 1))
+            const double x = (double)(lo - k);
+            rd[k] = (x * (tail + x)) / ((rr - x + 1.0) * (mm - x + 1.0));
         }
-        // out of support, or both tails below 1e-18 (the rest of the mass is rounding residue)
-        if (!moved || (phi < 1e-18 && plo < 1e-18)) return x0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bool moved = false;
+            if (hi < xmax) {
+                phi = phi * ru[k];
+                ++hi;
+                u = u - phi;
+                if (u < 0.0) return hi;
+                moved = true;
+            }
+            if (lo > xmin) {
+                plo = plo * rd[k];
+                --lo;
+                u = u - plo;
+                if (u < 0.0) return lo;
+                moved = true;
+            }
+            // out of support, or both tails below 1e-18 (the rest of the mass is rounding residue)
+            if (!moved || (phi < 1e-18 && plo < 1e-18)) return x0;
+        }
     }
 }
 
@@ -217,6 +245,30 @@ __host__ __device__ inline int64_t chunk_pop(int64_t a, int64_t b, int64_t d) { 
 }
 __host__ __device__ inline uint64_t tree_key(uint64_t ckey) { return mix64(ckey ^ 0x5851F42D4C957F2Dull); }
 
+__host__ __device__ inline uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// Few members (m <= SEQ_MAX): the m draws without replacement made one by one — draw s lands in the
+// left part with probability remL / remT, decided by the 64-bit uniform u_s as
+// floor(u_s remT / 2^64) < remL (exact up to 2^-64 per draw); integer arithmetic only.
+constexpr int64_t SEQ_MAX = 64;
+__host__ __device__ inline int64_t seq_draw(uint64_t nkey, int64_t N, int64_t r, int64_t m) {
+    uint64_t remT = (uint64_t)N, remL = (uint64_t)r;
+    int64_t x = 0;
+    for (int64_t s = 0; s < m; ++s) {
+        const uint64_t u = ((uint64_t)fmix32((uint32_t)nkey + 0x9E3779B1u * (uint32_t)(2 * s)) << 32) |
+                           fmix32((uint32_t)(nkey >> 32) + 0x9E3779B1u * (uint32_t)(2 * s + 1));
+        if (mulhi64(u, remT) < remL) { ++x; --remL; }
+        --remT;
+    }
+    return x;
+}
+
 // split of node (l, i) holding m members: the left child's count
 __host__ __device__ inline int64_t node_split(uint64_t tkey, int64_t C, int64_t d, int l, int64_t i, int64_t m) {
     if (m == 0) return 0;
@@ -224,7 +276,9 @@ __host__ __device__ inline int64_t node_split(uint64_t tkey, int64_t C, int64_t 
     const int64_t pl = chunk_pop(a, mid, d), pr = chunk_pop(mid, b, d);
     if (pl == 0) return 0;
     if (pr == 0) return m;
-    return hyper_draw(pl + pr, pl, m, uniform53(tkey, ((int64_t)1 << l) + i));
+    const int64_t node = ((int64_t)1 << l) + i;
+    if (m <= SEQ_MAX) return seq_draw(mix64(tkey ^ (0x9E3779B97F4A7C15ull * (uint64_t)node)), pl + pr, pl, m);
+    return hyper_draw(pl + pr, pl, m, uniform53(tkey, node));
 }
 
 // ---- the keyed permutation inside a chunk -----------------------------------------------------

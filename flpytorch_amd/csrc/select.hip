@@ -1166,8 +1166,19 @@ struct RkdWs {
     int64_t lstride;   // 2^L
 };
 
-__global__ __launch_bounds__(256) void k_randk_counts(int64_t n, int64_t d, int64_t K, uint64_t seed, int64_t client0,
-                                                      RkdWs ws) {
+// lists (optional): the chunk_accum view of the row — tab[c][row] = (offset, count) with the
+// members laid out chunk by chunk, and the F_EXACT row state (every listed entry is kept)
+struct RkLists {
+    uint2* tab;
+    uint32_t* thr;
+    uint32_t* flags;
+    uint32_t* rowcnt;
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_randk_counts(int64_t n, int64_t d, int64_t K, uint64_t seed, int64_t client0,
+                                                     RkdWs ws, RkLists ls) {
+    __shared__ uint32_t part[NT];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x;
     const uint64_t ck = client_key(seed, client0 + row);
@@ -1180,12 +1191,17 @@ __global__ __launch_bounds__(256) void k_randk_counts(int64_t n, int64_t d, int6
     if (tid == 0) {
         ws.ckey[row] = ck;
         H[1] = (uint32_t)K;
+        if (ls.tab) {
+            ls.thr[row] = 0;
+            ls.flags[row] = F_EXACT;          // the lists hold exactly the kept entries
+            ls.rowcnt[row * RCS] = (uint32_t)K;
+        }
     }
     __syncthreads();
     for (int l = 0; l < L; ++l) {
         const uint32_t* A = H + ((int64_t)1 << l);
         uint32_t* B = H + ((int64_t)2 << l);
-        for (int64_t i = tid; i < ((int64_t)1 << l); i += 256) {
+        for (int64_t i = tid; i < ((int64_t)1 << l); i += NT) {
             const int64_t m = A[i];
             const int64_t x = rktree::node_split(tk, C, d, l, i, m);
             B[2 * i] = (uint32_t)x;
@@ -1194,9 +1210,82 @@ __global__ __launch_bounds__(256) void k_randk_counts(int64_t n, int64_t d, int6
         __syncthreads();                                 // block-scope visibility of the level
     }
     const uint32_t* A = H + ((int64_t)1 << L);
-    for (int64_t i = tid; i < ((int64_t)1 << L); i += 256) {
+    const int64_t nl = (int64_t)1 << L, per = (nl + NT - 1) / NT;
+    const int64_t i0 = min(nl, tid * per), i1 = min(nl, i0 + per);
+    uint32_t loc = 0;
+    for (int64_t i = i0; i < i1; ++i) {
         const int64_t a = rktree::node_lo(C, L, i);
-        if (rktree::node_lo(C, L, i + 1) - a == 1) ws.cnt[a * n + row] = A[i];
+        if (rktree::node_lo(C, L, i + 1) - a == 1) {
+            ws.cnt[a * n + row] = A[i];
+            loc += A[i];
+        }
+    }
+    if (!ls.tab) return;
+    part[tid] = loc;                                   // exclusive scan of the threads' sums
+    __syncthreads();
+    for (int off = 1; off < NT; off <<= 1) {
+        const uint32_t v = tid >= off ? part[tid - off] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - loc;
+    for (int64_t i = i0; i < i1; ++i) {
+        const int64_t a = rktree::node_lo(C, L, i);
+        if (rktree::node_lo(C, L, i + 1) - a == 1) {
+            ls.tab[a * n + row] = make_uint2(run, A[i]);
+            run += A[i];
+        }
+    }
+}
+
+// Row-major member generation + gather: each wave takes RKG_CPW consecutive chunks of one row,
+// lane t < m_c writes member t of chunk c (its global index and (D/K) x[j]) at the row's list
+// position tab[c][row].x + t — the lists k_chunk_accum folds.  The gathers of a wave stay inside one
+// row's 16 KB windows, chunk after chunk (page- and DRAM-row-local, like the compat path's
+// k_randk_fine); the RKG_CPW chunks' loads are issued before any store.
+constexpr int RKG_CPW = 4;
+__global__ __launch_bounds__(256) void k_randk_gen(RowSrc rows, int64_t n, int64_t d, const uint64_t* __restrict__ ckey,
+                                                   float scale, SelWs ws) {
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t C = nchunks(d);
+    for (int64_t row = blockIdx.y; row < n; row += gridDim.y) {
+        const uint64_t k = ckey[row];
+        const float* r = rows.row_s(row);
+        uint32_t* oi = ws.ent_idx + row * ws.cap;
+        float* ov = ws.ent_val + row * ws.cap;
+        for (int64_t c0 = ((int64_t)blockIdx.x * 4 + wv) * RKG_CPW; c0 < C; c0 += (int64_t)gridDim.x * 4 * RKG_CPW) {
+            uint2 te[RKG_CPW];
+            uint32_t col[RKG_CPW];
+            float v[RKG_CPW];
+#pragma unroll
+            for (int q = 0; q < RKG_CPW; ++q) {
+                const int64_t c = c0 + q;
+                te[q] = c < C ? ws.tab[c * n + row] : make_uint2(0u, 0u);
+                const uint32_t clen = (uint32_t)min((int64_t)CHUNK, d - c * CHUNK);
+                const rktree::ChunkPerm P(k, c, clen);
+                col[q] = (uint32_t)lane < te[q].y ? P((uint32_t)lane) : 0u;
+                v[q] = (uint32_t)lane < te[q].y ? r[c * CHUNK + col[q]] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < RKG_CPW; ++q) {
+                const int64_t c = c0 + q;
+                if ((uint32_t)lane < te[q].y) {
+                    oi[te[q].x + lane] = (uint32_t)(c * CHUNK + col[q]);
+                    ov[te[q].x + lane] = scale * v[q];
+                }
+                if (te[q].y > 64u) {                      // a chunk with more than 64 members
+                    const uint32_t clen = (uint32_t)min((int64_t)CHUNK, d - c * CHUNK);
+                    const rktree::ChunkPerm P(k, c, clen);
+                    for (uint32_t t = 64u + lane; t < te[q].y; t += 64) {
+                        const uint32_t cc = P(t);
+                        oi[te[q].x + t] = (uint32_t)(c * CHUNK + cc);
+                        ov[te[q].x + t] = scale * r[c * CHUNK + cc];
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -1457,8 +1546,9 @@ size_t randk_device_workspace(int64_t n, int64_t d);
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     size_t b = 0;
     carve_sel(nullptr, prm->codec, n, d, prm->k, &b);
-    // RandK: the pattern (compat lists or device draws) is not known at the size query
-    if (prm->codec == FLC_RANDK) b = std::max(b, randk_device_workspace(n, d));
+    // RandK: the pattern (compat lists or device draws) is not known at the size query; device
+    // draws use the same lists plus the count tree
+    if (prm->codec == FLC_RANDK) b += randk_device_workspace(n, d);
     return b;
 }
 
@@ -1493,6 +1583,9 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream
     hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
 }
 
+static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
+                              hipStream_t st);
+
 static RkdWs carve_rkd(void* base, int64_t n, int64_t d, size_t* bytes) {
     Carver cv(base);
     const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
@@ -1512,10 +1605,12 @@ size_t randk_device_workspace(int64_t n, int64_t d) {
 }
 
 static int randk_counts(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d, RkdWs ws,
-                        hipStream_t st) {
+                        hipStream_t st, RkLists ls = RkLists{nullptr, nullptr, nullptr, nullptr}) {
     ProfScope _ps("k_randk_counts", st);
-    hipLaunchKernelGGL(k_randk_counts, dim3((unsigned)n), dim3(256), 0, st, n, d, prm->k, prm->seed,
-                       pat ? pat->client0 : (int64_t)0, ws);
+    // one 256-thread workgroup per row (1024 threads halve a lone row's latency but cost throughput
+    // at C5's 683 rows: 4.4 ms against 3.4 ms, measured)
+    hipLaunchKernelGGL(k_randk_counts<256>, dim3((unsigned)n), dim3(256), 0, st, n, d, prm->k, prm->seed,
+                       pat ? pat->client0 : (int64_t)0, ws, ls);
     FLC_CHECK_LAUNCH("k_randk_counts");
     return FLC_OK;
 }
@@ -1539,33 +1634,59 @@ int randk_device_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, in
 // device-RNG RandK encode + reduce: counts, then the list-free chunk fold
 int randk_device_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d,
                      const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
-    if (ws_bytes < randk_device_workspace(n, d)) { set_error("randk: workspace too small"); return FLC_ERR_WORKSPACE; }
-    RkdWs ws = carve_rkd(wsp, n, d, nullptr);
-    if (int rc = randk_counts(prm, pat, n, d, ws, st)) return rc;
+    size_t lb = 0;
+    carve_sel(nullptr, FLC_RANDK, n, d, prm->k, &lb);
+    if (ws_bytes < lb + randk_device_workspace(n, d)) { set_error("randk: workspace too small"); return FLC_ERR_WORKSPACE; }
+    SelWs sw = carve_sel(wsp, FLC_RANDK, n, d, prm->k, nullptr);
+    RkdWs rw = carve_rkd(static_cast<char*>(wsp) + lb, n, d, nullptr);
     const int64_t C = host_chunks(d);
-    // few chunks (short rows: C2's D = 1 M has 245): each chunk's columns over up to 16 waves, so
-    // the row-serial walk runs on ~8 K waves (each wave still regenerates all of a row's members of
-    // the chunk, but gathers only those in its part)
-    int parts = 1;
-    while (parts < 16 && parts * C < 8192) parts *= 2;
-    const int ab = grid_stride_blocks((parts * C + 3) / 4, 16384);
-    ProfScope _ps("k_randk_fold", st);
-    if (parts == 16)
-        hipLaunchKernelGGL((k_randk_fold<CHUNK / 16>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
+    // Long rows (>= 1024 chunks, one wave per chunk fills the chip): the list-free chunk fold, each
+    // wave regenerating the rows' members of its chunk.  Short rows: too few chunks for the
+    // row-serial fold, so the members are written per row (k_randk_gen) and the chunk fold runs
+    // over the lists with its column split (k_chunk_accum).
+    if (C >= 1024) {
+        if (int rc = randk_counts(prm, pat, n, d, rw, st)) return rc;
+        ProfScope _ps("k_randk_fold", st);
+        const int ab = grid_stride_blocks((C + 3) / 4, 16384);
+        hipLaunchKernelGGL((k_randk_fold<CHUNK>), dim3(ab), dim3(256), 0, st, rows, n, d, rw.cnt, rw.ckey,
                            prm->randk_scale, w, wt, out);
-    else if (parts == 8)
-        hipLaunchKernelGGL((k_randk_fold<CHUNK / 8>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
-                           prm->randk_scale, w, wt, out);
-    else if (parts == 4)
-        hipLaunchKernelGGL((k_randk_fold<CHUNK / 4>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
-                           prm->randk_scale, w, wt, out);
-    else if (parts == 2)
-        hipLaunchKernelGGL((k_randk_fold<CHUNK / 2>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
-                           prm->randk_scale, w, wt, out);
-    else
-        hipLaunchKernelGGL((k_randk_fold<CHUNK>), dim3(ab), dim3(256), 0, st, rows, n, d, ws.cnt, ws.ckey,
-                           prm->randk_scale, w, wt, out);
-    FLC_CHECK_LAUNCH("k_randk_fold");
+        FLC_CHECK_LAUNCH("k_randk_fold");
+        return FLC_OK;
+    }
+    if (int rc = randk_counts(prm, pat, n, d, rw, st, RkLists{sw.tab, sw.thr, sw.flags, sw.rowcnt})) return rc;
+    {
+        ProfScope _ps("k_randk_gen", st);
+        const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((C + 4 * RKG_CPW - 1) / (4 * RKG_CPW), 4096));
+        hipLaunchKernelGGL(k_randk_gen, dim3((unsigned)gx, (unsigned)std::min<int64_t>(n, 65535)), dim3(256), 0, st, rows,
+                           n, d, rw.ckey, prm->randk_scale, sw);
+        FLC_CHECK_LAUNCH("k_randk_gen");
+    }
+    return launch_chunk_accum(n, d, sw, false, w, wt, out, st);
+}
+
+// chunk-owner fold of the rows' lists (TopK candidates, RandK members)
+static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
+                              hipStream_t st) {
+    const int64_t C = host_chunks(d);
+    { ProfScope _ps("k_chunk_accum", st);
+    // few chunks (short rows: C2's D = 1 M has 245): split each chunk's columns over 2 or 4 waves so
+    // the latency-bound row walk runs on more of the chip (many chunks: one wave each, measured best)
+    int parts = accum_parts();
+    if (parts == 0) parts = C >= 1024 ? 1 : (C >= 256 ? 2 : 4);
+    if (parts == 4) {
+        const int ab = grid_stride_blocks((4 * C + 3) / 4, 8192);
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    } else if (parts == 2) {
+        const int ab = grid_stride_blocks((2 * C + 3) / 4, 8192);
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    } else {
+        const int ab = grid_stride_blocks((C + 3) / 4, 4096);
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    } }
+    FLC_CHECK_LAUNCH("k_chunk_accum");
     return FLC_OK;
 }
 
@@ -1655,26 +1776,7 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
         FLC_CHECK_LAUNCH("k_assign_scatter");
         return FLC_OK;
     }
-    { ProfScope _ps("k_chunk_accum", st);
-    // few chunks (short rows: C2's D = 1 M has 245): split each chunk's columns over 2 or 4 waves so
-    // the latency-bound row walk runs on more of the chip (many chunks: one wave each, measured best)
-    int parts = accum_parts();
-    if (parts == 0) parts = C >= 1024 ? 1 : (C >= 256 ? 2 : 4);
-    if (parts == 4) {
-        const int ab = grid_stride_blocks((4 * C + 3) / 4, 8192);
-        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    } else if (parts == 2) {
-        const int ab = grid_stride_blocks((2 * C + 3) / 4, 8192);
-        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    } else {
-        const int ab = grid_stride_blocks((C + 3) / 4, 4096);
-        if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    } }
-    FLC_CHECK_LAUNCH("k_chunk_accum");
-    return FLC_OK;
+    return launch_chunk_accum(n, d, ws, assign, w, wt, out, st);
 }
 
 // ------------------------------------------------------------------------------------------

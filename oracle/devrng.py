@@ -132,15 +132,18 @@ def _stirlerr(n):
     return (S0 - (S1 - (S2 - (S3 - S4 / nn) / nn) / nn) / nn) / n
 
 
+_BD0_R = [1.0 / (2 * j + 1) for j in range(1, 25)]
+
+
 def _bd0(x, np_):
     if abs(x - np_) < 0.1 * (x + np_):
         v = (x - np_) / (x + np_)
         s = (x - np_) * v
         ej = 2.0 * x * v
         v = v * v
-        for j in range(1, 1000):
+        for rj in _BD0_R:
             ej = ej * v
-            s1 = s + ej / float(2 * j + 1)
+            s1 = s + ej * rj
             if s1 == s:
                 return s1
             s = s1
@@ -173,8 +176,17 @@ def dhyper(x, r, b, m):
         return 0.0
     if m == 0.0:
         return 1.0 if x == 0.0 else 0.0
-    p, q = m / (r + b), (r + b - m) / (r + b)
-    return _dbinom_raw(x, r, p, q) * _dbinom_raw(m - x, b, p, q) / _dbinom_raw(m, r + b, p, q)
+    N = r + b
+    p, q = m / N, (N - m) / N
+    y = m - x
+    z = b - y
+    if x == 0.0 or x == r or y == 0.0 or z == 0.0 or m == N:
+        return _dbinom_raw(x, r, p, q) * _dbinom_raw(y, b, p, q) / _dbinom_raw(m, N, p, q)
+    lc = ((_stirlerr(r) - _stirlerr(x) - _stirlerr(r - x) - _bd0(x, r * p) - _bd0(r - x, r * q)) +
+          (_stirlerr(b) - _stirlerr(y) - _stirlerr(z) - _bd0(y, b * p) - _bd0(z, b * q)) -
+          (_stirlerr(N) - _stirlerr(m) - _stirlerr(N - m) - _bd0(m, N * p) - _bd0(N - m, N * q)))
+    lf = _LN_2PI + _dlog(((x * (r - x)) / r) * ((y * z) / b) * (N / (m * (N - m))))
+    return _dexp(lc - 0.5 * lf)
 
 
 def hyper_draw(N, r, m, u):
@@ -234,6 +246,32 @@ def _pop(a, b, d):
     return min(b * _CH, d) - a * _CH
 
 
+_SEQ_MAX = 64
+
+
+def _fmix32_int(h):
+    h &= 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+def seq_draw(nkey, N, r, m):
+    """Few members: the m draws one by one, draw s left iff floor(u_s remT / 2^64) < remL."""
+    remT, remL, x = N, r, 0
+    lo, hi = nkey & 0xFFFFFFFF, nkey >> 32
+    for s in range(m):
+        u = (_fmix32_int(lo + 0x9E3779B1 * (2 * s)) << 32) | _fmix32_int(hi + 0x9E3779B1 * (2 * s + 1))
+        if (u * remT) >> 64 < remL:
+            x += 1
+            remL -= 1
+        remT -= 1
+    return x
+
+
 def randk_counts(seed, client, d, k):
     """Members of the client's device RandK set in each 4096-element chunk (int64[C])."""
     ck = client_key(seed, client)
@@ -249,7 +287,15 @@ def randk_counts(seed, client, d, k):
             if m:
                 a, mid, b = (i * C) >> l, ((2 * i + 1) * C) >> (l + 1), ((i + 1) * C) >> l
                 pl, pr = _pop(a, mid, d), _pop(mid, b, d)
-                x = 0 if pl == 0 else (m if pr == 0 else hyper_draw(pl + pr, pl, m, _uniform53(tk, (1 << l) + i)))
+                node = (1 << l) + i
+                if pl == 0:
+                    x = 0
+                elif pr == 0:
+                    x = m
+                elif m <= _SEQ_MAX:
+                    x = seq_draw(_mix64(tk ^ ((0x9E3779B97F4A7C15 * node) & _M64)), pl + pr, pl, m)
+                else:
+                    x = hyper_draw(pl + pr, pl, m, _uniform53(tk, node))
             nxt[2 * i], nxt[2 * i + 1] = x, m - x
         cur = nxt
     cnt = np.zeros(C, dtype=np.int64)

@@ -23,8 +23,12 @@ def timed(fn, reps=10):
 
 
 lib = _lib.load()
-for n, d, k, label in [(256, 1_000_000, 10_000, "c2"), (683, 100_000_000, 1_000_000, "c5-randk"),
-                       (64, 10_000_000, 100_000, "mid")]:
+SHAPES = [(256, 1_000_000, 10_000, "c2"), (683, 100_000_000, 1_000_000, "c5-randk"),
+          (64, 10_000_000, 100_000, "mid")]
+if len(sys.argv) > 1 and sys.argv[1] == "counts":
+    SHAPES = [(1, 1_000_000, 10_000, "c2x1"), (16, 1_000_000, 10_000, "c2x16"), (1, 100_000_000, 1_000_000, "c5x1"),
+              (64, 100_000_000, 1_000_000, "c5x64"), (1, 1_000_000, 100, "c2-k100"), (1, 4096 * 256, 256 * 41, "L8")]
+for n, d, k, label in SHAPES:
     C = (d + 4095) // 4096
     out = torch.zeros((C, n), dtype=torch.int32, device="cuda")
     wsb = lib.flc_device_randk_counts_workspace_size(n, d)
@@ -34,6 +38,9 @@ for n, d, k, label in [(256, 1_000_000, 10_000, "c2"), (683, 100_000_000, 1_000_
         assert lib.flc_device_randk_counts(7, 0, n, d, k, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
                                            wsb, _lib.stream_ptr()) == 0
     res = {"shape": label, "n": n, "d": d, "k": k, "counts_ms": round(timed(counts), 4)}
+    if len(sys.argv) > 1:
+        print(json.dumps(res), flush=True)
+        continue
     if d * n * 4 < 40e9:
         rows = torch.randn(n, d, device="cuda")
         red = ag.UplinkReducer(ag.initCompressor(f"randk:{k}", d), seed=7)
