@@ -363,6 +363,8 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--row-groups", type=int, default=None,
+                    help="sparse QSGD / TopK execution hint: fold row group g while group g+1 is filtered")
     ap.add_argument("--compat", action="store_true",
                     help="compat-mode patterns: the reference's numpy-stream RandK indices / dithering uniforms, "
                          "resident in HBM and read by the kernels (their bytes counted)")
@@ -486,7 +488,10 @@ def main():
         if world > 1:
             group = dist.group.WORLD
     else:
-        red = ag.UplinkReducer(ag.initCompressor(spec, d), device=dev, seed=20241015)
+        comp = ag.initCompressor(spec, d)
+        if args.row_groups:
+            comp.row_groups = args.row_groups      # execution hint: the fold of row group g under group g+1's pass
+        red = ag.UplinkReducer(comp, device=dev, seed=20241015)
 
     if strong:
         uplink = ShardedUplink(product_partial(red), group=dist.group.WORLD if world > 1 else None, mode="ordered",

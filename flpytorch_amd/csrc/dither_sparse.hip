@@ -562,10 +562,13 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
 // A/B switches once per process (FLC_DS_GCAP=1024 doubles the per-item staging and list regions,
 // FLC_DS_GRID=res launches a resident-only grid, FLC_DS_FGS=4 four-chunk items), so the
 // workspace query and the run always see the same variant.
-struct DsVariant { int gcap; bool resident; int ap; int fgs; int probe; int aprobe; };
+struct DsVariant { int gcap; bool resident; int ap; int fgs; int probe; int aprobe; int gridpct; };
 static const DsVariant& ds_variant() {
     static const DsVariant v = [] {
-        DsVariant r{DS_GCAP, false, DS_AP, DS_FGS, 0, 0};
+        DsVariant r{DS_GCAP, false, DS_AP, DS_FGS, 0, 0, 100};
+        // FLC_DS_GRIDPCT=p: with row groups, the filter grid is capped at p % of the resident
+        // blocks so the previous group's fold finds free slots beside it
+        if (const char* e = tuning_env("FLC_DS_GRIDPCT")) r.gridpct = std::max(10, std::min(100, atoi(e)));
         if (const char* e = tuning_env("FLC_DS_FGS")) r.fgs = atoi(e) == 4 ? 4 : DS_FGS;
         if (const char* e = tuning_env("FLC_DS_AP")) r.ap = atoi(e);
         if (const char* e = tuning_env("FLC_DS_GCAP")) r.gcap = atoi(e) == 1024 ? 1024 : DS_GCAP;
@@ -657,12 +660,12 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     auto filter = [&](int64_t r0, int64_t rn) -> int {
         auto launch = [&](auto kern) {
             int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
-            if (v.resident) {
+            if (v.resident || (K > 1 && v.gridpct < 100)) {
                 int per = 0, dev = 0, cus = 0;
                 if (hipGetDevice(&dev) == hipSuccess &&
                     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
                     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) == hipSuccess && per > 0)
-                    gw = std::min(gw, per * cus);
+                    gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
             }
             ProfScope _ps("k_ds_filter", st);
             hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, d, ws);

@@ -166,30 +166,19 @@ extern "C" int flc_device_randk_indices(uint64_t seed, int64_t client, int64_t d
         flc::set_error("flc_device_randk_indices: bad arguments");
         return FLC_ERR_ARG;
     }
-    // host mirror of k_randk_counts + the chunk permutations (randk_tree.hpp): chunk by chunk,
-    // within a chunk in permutation order
+    // host mirror of k_randk_counts (histogram of the row permutation's first k images by chunk)
+    // + the chunk permutations: chunk by chunk, within a chunk in permutation order
     namespace rt = flc::rktree;
     const uint64_t ck = flc::client_key(seed, client);
     const int64_t C = (d + rt::CH - 1) / rt::CH;
-    const int L = rt::tree_depth(C);
-    const uint64_t tk = rt::tree_key(ck);
-    std::vector<int64_t> cur(1, k), nxt;
-    for (int l = 0; l < L; ++l) {
-        nxt.assign((size_t)2 << l, 0);
-        for (int64_t i = 0; i < ((int64_t)1 << l); ++i) {
-            const int64_t x = rt::node_split(tk, C, d, l, i, cur[i]);
-            nxt[2 * i] = x;
-            nxt[2 * i + 1] = cur[i] - x;
-        }
-        cur.swap(nxt);
-    }
+    std::vector<int64_t> cnt((size_t)C, 0);
+    const rt::RowPerm P(ck, (uint64_t)d);
+    for (int64_t t = 0; t < k; ++t) ++cnt[(size_t)(P((uint64_t)t) >> rt::CH_SHIFT)];
     int64_t pos = 0;
-    for (int64_t i = 0; i < ((int64_t)1 << L); ++i) {
-        const int64_t c = rt::node_lo(C, L, i);
-        if (rt::node_lo(C, L, i + 1) - c != 1) continue;
+    for (int64_t c = 0; c < C; ++c) {
         const uint32_t clen = (uint32_t)std::min<int64_t>(rt::CH, d - c * rt::CH);
-        const rt::ChunkPerm P(ck, c, clen);
-        for (int64_t t = 0; t < cur[i]; ++t) h_out[pos++] = c * rt::CH + P((uint32_t)t);
+        const rt::ChunkPerm Q(ck, c, clen);
+        for (int64_t t = 0; t < cnt[(size_t)c]; ++t) h_out[pos++] = c * rt::CH + Q((uint32_t)t);
     }
     return pos == k ? FLC_OK : FLC_ERR_ARG;
 }

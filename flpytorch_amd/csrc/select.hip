@@ -1162,80 +1162,76 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
 struct RkdWs {
     uint32_t* cnt;     // [C][N]
     uint64_t* ckey;    // [N]
-    uint32_t* lev;     // [N][2^(L+1)] tree levels (heap layout)
-    int64_t lstride;   // 2^L
 };
 
-// lists (optional): the chunk_accum view of the row — tab[c][row] = (offset, count) with the
-// members laid out chunk by chunk, and the F_EXACT row state (every listed entry is kept)
-struct RkLists {
-    uint2* tab;
-    uint32_t* thr;
-    uint32_t* flags;
-    uint32_t* rowcnt;
-};
+// Chunk counts of the device sampler (randk_tree.hpp): each workgroup takes one row and a range of
+// RKC_BINS chunks, evaluates Pi(t) for all t < K with a persistent cycle walk (every lane does
+// useful work each trip) and histograms the chunk ids in LDS (16-bit bins: a chunk holds <= 4096).
+constexpr int RKC_NT = 1024;
+constexpr int64_t RKC_BINS = 32768;
 
-template <int NT>
-__global__ __launch_bounds__(NT) void k_randk_counts(int64_t n, int64_t d, int64_t K, uint64_t seed, int64_t client0,
-                                                     RkdWs ws, RkLists ls) {
-    __shared__ uint32_t part[NT];
+__global__ __launch_bounds__(RKC_NT) void k_randk_counts(int64_t n, int64_t d, int64_t K, uint64_t seed, int64_t client0,
+                                                         RkdWs ws) {
+    __shared__ uint32_t bins[RKC_BINS / 2];
+    const int64_t row = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int64_t C = nchunks(d);
+    const int64_t c0 = (int64_t)blockIdx.x * RKC_BINS, nc = min(C, c0 + RKC_BINS) - c0;
+    const uint64_t ck = client_key(seed, client0 + row);
+    for (int64_t i = tid; i < (nc + 1) / 2; i += RKC_NT) bins[i] = 0;
+    __syncthreads();
+    const rktree::RowPerm P(ck, (uint64_t)d);
+    int64_t t = tid;
+    bool live = t < K;
+    uint64_t x = (uint64_t)t;
+    while (__ballot(live) != 0ull) {
+        const uint64_t v = P.once(x);
+        if (live) {
+            if (v < (uint64_t)d) {
+                const int64_t c = (int64_t)(v >> CHUNK_SHIFT) - c0;
+                if ((uint64_t)c < (uint64_t)nc) atomicAdd(&bins[c >> 1], 1u << (16 * (c & 1)));
+                t += RKC_NT;
+                live = t < K;
+                x = (uint64_t)t;
+            } else {
+                x = v;
+            }
+        }
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) ws.ckey[row] = ck;
+    for (int64_t c = tid; c < nc; c += RKC_NT) ws.cnt[(c0 + c) * n + row] = (bins[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+}
+
+// lists view of the counts (the short-row path): tab[c][row] = (offset, count) with the members
+// laid out chunk by chunk, and the F_EXACT row state (every listed entry is kept)
+__global__ __launch_bounds__(256) void k_randk_tab(int64_t n, int64_t d, int64_t K, const uint32_t* __restrict__ cnt,
+                                                   SelWs ls) {
+    __shared__ uint32_t part[256];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x;
-    const uint64_t ck = client_key(seed, client0 + row);
-    const int64_t C = nchunks(d);
-    const int L = rktree::tree_depth(C);
-    const uint64_t tk = rktree::tree_key(ck);
-    // heap layout: level l at [2^l, 2^(l+1)) — every word is written once and read only after the
-    // barrier that follows its write (no line of it can sit stale in the CU's L1)
-    uint32_t* H = ws.lev + row * 2 * ws.lstride;
-    if (tid == 0) {
-        ws.ckey[row] = ck;
-        H[1] = (uint32_t)K;
-        if (ls.tab) {
-            ls.thr[row] = 0;
-            ls.flags[row] = F_EXACT;          // the lists hold exactly the kept entries
-            ls.rowcnt[row * RCS] = (uint32_t)K;
-        }
-    }
-    __syncthreads();
-    for (int l = 0; l < L; ++l) {
-        const uint32_t* A = H + ((int64_t)1 << l);
-        uint32_t* B = H + ((int64_t)2 << l);
-        for (int64_t i = tid; i < ((int64_t)1 << l); i += NT) {
-            const int64_t m = A[i];
-            const int64_t x = rktree::node_split(tk, C, d, l, i, m);
-            B[2 * i] = (uint32_t)x;
-            B[2 * i + 1] = (uint32_t)(m - x);
-        }
-        __syncthreads();                                 // block-scope visibility of the level
-    }
-    const uint32_t* A = H + ((int64_t)1 << L);
-    const int64_t nl = (int64_t)1 << L, per = (nl + NT - 1) / NT;
-    const int64_t i0 = min(nl, tid * per), i1 = min(nl, i0 + per);
+    const int64_t C = nchunks(d), per = (C + 255) / 256;
+    const int64_t c0 = min(C, tid * per), c1 = min(C, c0 + per);
     uint32_t loc = 0;
-    for (int64_t i = i0; i < i1; ++i) {
-        const int64_t a = rktree::node_lo(C, L, i);
-        if (rktree::node_lo(C, L, i + 1) - a == 1) {
-            ws.cnt[a * n + row] = A[i];
-            loc += A[i];
-        }
-    }
-    if (!ls.tab) return;
-    part[tid] = loc;                                   // exclusive scan of the threads' sums
+    for (int64_t c = c0; c < c1; ++c) loc += cnt[c * n + row];
+    part[tid] = loc;
     __syncthreads();
-    for (int off = 1; off < NT; off <<= 1) {
+    for (int off = 1; off < 256; off <<= 1) {
         const uint32_t v = tid >= off ? part[tid - off] : 0u;
         __syncthreads();
         part[tid] += v;
         __syncthreads();
     }
     uint32_t run = part[tid] - loc;
-    for (int64_t i = i0; i < i1; ++i) {
-        const int64_t a = rktree::node_lo(C, L, i);
-        if (rktree::node_lo(C, L, i + 1) - a == 1) {
-            ls.tab[a * n + row] = make_uint2(run, A[i]);
-            run += A[i];
-        }
+    for (int64_t c = c0; c < c1; ++c) {
+        const uint32_t m = cnt[c * n + row];
+        ls.tab[c * n + row] = make_uint2(run, m);
+        run += m;
+    }
+    if (tid == 0) {
+        ls.thr[row] = 0;
+        ls.flags[row] = F_EXACT;
+        ls.rowcnt[row * RCS] = (uint32_t)K;
     }
 }
 
@@ -1590,10 +1586,8 @@ static RkdWs carve_rkd(void* base, int64_t n, int64_t d, size_t* bytes) {
     Carver cv(base);
     const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
     RkdWs s;
-    s.lstride = (int64_t)1 << rktree::tree_depth(C);
     s.cnt = cv.take<uint32_t>((size_t)C * nn);
     s.ckey = cv.take<uint64_t>((size_t)nn);
-    s.lev = cv.take<uint32_t>((size_t)nn * 2 * s.lstride);
     if (bytes) *bytes = cv.bytes();
     return s;
 }
@@ -1605,12 +1599,11 @@ size_t randk_device_workspace(int64_t n, int64_t d) {
 }
 
 static int randk_counts(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d, RkdWs ws,
-                        hipStream_t st, RkLists ls = RkLists{nullptr, nullptr, nullptr, nullptr}) {
+                        hipStream_t st) {
     ProfScope _ps("k_randk_counts", st);
-    // one 256-thread workgroup per row (1024 threads halve a lone row's latency but cost throughput
-    // at C5's 683 rows: 4.4 ms against 3.4 ms, measured)
-    hipLaunchKernelGGL(k_randk_counts<256>, dim3((unsigned)n), dim3(256), 0, st, n, d, prm->k, prm->seed,
-                       pat ? pat->client0 : (int64_t)0, ws, ls);
+    const int64_t parts = (host_chunks(d) + RKC_BINS - 1) / RKC_BINS;
+    hipLaunchKernelGGL(k_randk_counts, dim3((unsigned)parts, (unsigned)n), dim3(RKC_NT), 0, st, n, d, prm->k, prm->seed,
+                       pat ? pat->client0 : (int64_t)0, ws);
     FLC_CHECK_LAUNCH("k_randk_counts");
     return FLC_OK;
 }
@@ -1653,7 +1646,9 @@ int randk_device_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc
         FLC_CHECK_LAUNCH("k_randk_fold");
         return FLC_OK;
     }
-    if (int rc = randk_counts(prm, pat, n, d, rw, st, RkLists{sw.tab, sw.thr, sw.flags, sw.rowcnt})) return rc;
+    if (int rc = randk_counts(prm, pat, n, d, rw, st)) return rc;
+    hipLaunchKernelGGL(k_randk_tab, dim3((unsigned)n), dim3(256), 0, st, n, d, prm->k, rw.cnt, sw);
+    FLC_CHECK_LAUNCH("k_randk_tab");
     {
         ProfScope _ps("k_randk_gen", st);
         const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((C + 4 * RKG_CPW - 1) / (4 * RKG_CPW), 4096));

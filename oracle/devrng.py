@@ -71,239 +71,46 @@ def uniforms(seed, client, d):
 
 
 # ---------------------------------------------------------------------------------------------
-# RandK device sampler (flpytorch_amd/csrc/randk_tree.hpp), restated op for op in Python floats
-# (IEEE doubles: +, -, *, / correctly rounded; frexp / ldexp / floor exact), so the counts and the
-# index sets equal the kernels' bit for bit.
-#   counts : a hypergeometric tree over the 4096-element chunks, node (l, i) = chunks
-#            [floor(i C / 2^l), floor((i + 1) C / 2^l)), split by inverting Loader's dhyper from one
-#            53-bit uniform keyed by (tree key, 2^l + i)
+# RandK device sampler (flpytorch_amd/csrc/randk_tree.hpp), restated in numpy integer arithmetic:
+#   counts : m_c = #{t < K : Pi(t) in chunk c}, Pi the row permutation of [0, D) (balanced 4-round
+#            Feistel on 2h bits, round keys from the client key, cycle-walked into [0, D))
 #   members: the first m_c images of a 4-round 6+6-bit Feistel permutation keyed by (client, c)
 # ---------------------------------------------------------------------------------------------
-import math
-
 _CH = 4096
-_LN2_HI = 6.93147180369123816490e-01
-_LN2_LO = 1.90821492927058770002e-10
-_LN_2PI = 1.8378770664093456
-_STIRLERR = [0.0, 0.08106146679532726, 0.0413406959554093, 0.02767792568499834, 0.020790672103765093,
-             0.016644691189821193, 0.013876128823070748, 0.01189670994589177, 0.010411265261972096,
-             0.009255462182712733, 0.00833056343336287, 0.007573675487951841, 0.00694284010720953,
-             0.006408994188004207, 0.0059513701127588475, 0.005554733551962801]
 
 
-def _dlog(x):
-    m, e = math.frexp(x)
-    if m < 0.70710678118654752440:
-        m = m * 2.0
-        e = e - 1
-    s = (m - 1.0) / (m + 1.0)
-    z = s * s
-    p = 1.0 / 25.0
-    for k in (23, 21, 19, 17, 15, 13, 11, 9, 7, 5, 3):
-        p = p * z + 1.0 / k
-    lm = 2.0 * s + 2.0 * s * (z * p)
-    de = float(e)
-    return de * _LN2_HI + (lm + de * _LN2_LO)
+def row_perm(ckey, d, t):
+    """Pi(t) for a uint64 array t (all < d)."""
+    b = 1
+    while (1 << (2 * b)) < d:
+        b += 1
+    mask = np.uint64((1 << b) - 1)
+    k = _mix64(ckey ^ 0x5851F42D4C957F2D)
+    rkey = [np.uint32(_mix64((k + (i << 56)) & _M64) & 0xFFFFFFFF) for i in range(4)]
+    sh = np.uint64(b)
 
+    def once(v):
+        l = ((v >> sh) & mask).astype(np.uint32)
+        r = (v & mask).astype(np.uint32)
+        m32 = np.uint32(int(mask))
+        for rk in rkey:
+            l, r = r, l ^ (fmix32(r ^ rk) & m32)
+        return (l.astype(np.uint64) << sh) | r.astype(np.uint64)
 
-def _dexp(x):
-    if not (x > -745.0):
-        return 0.0
-    kf = math.floor(x * 1.4426950408889634 + 0.5)
-    r = (x - kf * _LN2_HI) - kf * _LN2_LO
-    p = 1.0
-    for i in range(18, 1, -1):
-        p = 1.0 + (r * p) * (1.0 / i)
-    p = 1.0 + r * p
-    return math.ldexp(p, int(kf))
-
-
-def _stirlerr(n):
-    if n <= 15.0:
-        return _STIRLERR[int(n)]
-    S0, S1, S2, S3, S4 = 1.0 / 12.0, 1.0 / 360.0, 1.0 / 1260.0, 1.0 / 1680.0, 1.0 / 1188.0
-    nn = n * n
-    if n > 500.0:
-        return (S0 - S1 / nn) / n
-    if n > 80.0:
-        return (S0 - (S1 - S2 / nn) / nn) / n
-    if n > 35.0:
-        return (S0 - (S1 - (S2 - S3 / nn) / nn) / nn) / n
-    return (S0 - (S1 - (S2 - (S3 - S4 / nn) / nn) / nn) / nn) / n
-
-
-_BD0_R = [1.0 / (2 * j + 1) for j in range(1, 25)]
-
-
-def _bd0(x, np_):
-    if abs(x - np_) < 0.1 * (x + np_):
-        v = (x - np_) / (x + np_)
-        s = (x - np_) * v
-        ej = 2.0 * x * v
-        v = v * v
-        for rj in _BD0_R:
-            ej = ej * v
-            s1 = s + ej * rj
-            if s1 == s:
-                return s1
-            s = s1
-        return s
-    return x * _dlog(x / np_) + np_ - x
-
-
-def _dbinom_raw(x, n, p, q):
-    if p == 0.0:
-        return 1.0 if x == 0.0 else 0.0
-    if q == 0.0:
-        return 1.0 if x == n else 0.0
-    if x == 0.0:
-        if n == 0.0:
-            return 1.0
-        return _dexp(-_bd0(n, n * q) - n * p if p < 0.1 else n * _dlog(q))
-    if x == n:
-        return _dexp(-_bd0(n, n * p) - n * q if q < 0.1 else n * _dlog(p))
-    if x < 0.0 or x > n:
-        return 0.0
-    lc = _stirlerr(n) - _stirlerr(x) - _stirlerr(n - x) - _bd0(x, n * p) - _bd0(n - x, n * q)
-    lf = _LN_2PI + _dlog(x) + _dlog((n - x) / n)
-    return _dexp(lc - 0.5 * lf)
-
-
-def dhyper(x, r, b, m):
-    """P(X = x): successes among m draws without replacement from r successes, b failures."""
-    x, r, b, m = float(x), float(r), float(b), float(m)
-    if x < 0.0 or m < x or r < x or m - x > b:
-        return 0.0
-    if m == 0.0:
-        return 1.0 if x == 0.0 else 0.0
-    N = r + b
-    p, q = m / N, (N - m) / N
-    y = m - x
-    z = b - y
-    if x == 0.0 or x == r or y == 0.0 or z == 0.0 or m == N:
-        return _dbinom_raw(x, r, p, q) * _dbinom_raw(y, b, p, q) / _dbinom_raw(m, N, p, q)
-    lc = ((_stirlerr(r) - _stirlerr(x) - _stirlerr(r - x) - _bd0(x, r * p) - _bd0(r - x, r * q)) +
-          (_stirlerr(b) - _stirlerr(y) - _stirlerr(z) - _bd0(y, b * p) - _bd0(z, b * q)) -
-          (_stirlerr(N) - _stirlerr(m) - _stirlerr(N - m) - _bd0(m, N * p) - _bd0(N - m, N * q)))
-    lf = _LN_2PI + _dlog(((x * (r - x)) / r) * ((y * z) / b) * (N / (m * (N - m))))
-    return _dexp(lc - 0.5 * lf)
-
-
-def hyper_draw(N, r, m, u):
-    if m <= 0 or r <= 0:
-        return 0
-    if r >= N:
-        return m
-    if m >= N:
-        return r
-    xmin, xmax = max(m - (N - r), 0), min(r, m)
-    if xmin >= xmax:
-        return xmin
-    x0 = int(math.floor((float(m) + 1.0) * (float(r) + 1.0) / (float(N) + 2.0)))
-    x0 = min(max(x0, xmin), xmax)
-    b, rr, mm, tail = float(N - r), float(r), float(m), float(N - r - m)
-    p0 = dhyper(x0, rr, b, mm)
-    u = u - p0
-    if u < 0.0:
-        return x0
-    lo = hi = x0
-    plo = phi = p0
-    while True:
-        moved = False
-        if hi < xmax:
-            x = float(hi)
-            phi = phi * (((rr - x) * (mm - x)) / ((x + 1.0) * (tail + x + 1.0)))
-            hi += 1
-            u = u - phi
-            if u < 0.0:
-                return hi
-            moved = True
-        if lo > xmin:
-            x = float(lo)
-            plo = plo * ((x * (tail + x)) / ((rr - x + 1.0) * (mm - x + 1.0)))
-            lo -= 1
-            u = u - plo
-            if u < 0.0:
-                return lo
-            moved = True
-        if not moved or (phi < 1e-18 and plo < 1e-18):
-            return x0
-
-
-def _uniform53(ckey, j):
-    z = _mix64((ckey + 0x9E3779B97F4A7C15 * j) & _M64)
-    return float(z >> 11) * (1.0 / 9007199254740992.0)
-
-
-def _tree_depth(C):
-    L = 0
-    while (1 << L) < C:
-        L += 1
-    return L
-
-
-def _pop(a, b, d):
-    return min(b * _CH, d) - a * _CH
-
-
-_SEQ_MAX = 64
-
-
-def _fmix32_int(h):
-    h &= 0xFFFFFFFF
-    h ^= h >> 16
-    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
-    h ^= h >> 13
-    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
-    h ^= h >> 16
-    return h
-
-
-def seq_draw(nkey, N, r, m):
-    """Few members: the m draws one by one, draw s left iff floor(u_s remT / 2^64) < remL."""
-    remT, remL, x = N, r, 0
-    lo, hi = nkey & 0xFFFFFFFF, nkey >> 32
-    for s in range(m):
-        u = (_fmix32_int(lo + 0x9E3779B1 * (2 * s)) << 32) | _fmix32_int(hi + 0x9E3779B1 * (2 * s + 1))
-        if (u * remT) >> 64 < remL:
-            x += 1
-            remL -= 1
-        remT -= 1
-    return x
+    v = once(np.asarray(t, dtype=np.uint64))
+    bad = v >= np.uint64(d)
+    while bad.any():
+        v[bad] = once(v[bad])
+        bad = v >= np.uint64(d)
+    return v
 
 
 def randk_counts(seed, client, d, k):
     """Members of the client's device RandK set in each 4096-element chunk (int64[C])."""
     ck = client_key(seed, client)
     C = (d + _CH - 1) // _CH
-    L = _tree_depth(C)
-    tk = _mix64(ck ^ 0x5851F42D4C957F2D)
-    cur = [k]
-    for l in range(L):
-        nxt = [0] * (2 << l)
-        for i in range(1 << l):
-            m = cur[i]
-            x = 0
-            if m:
-                a, mid, b = (i * C) >> l, ((2 * i + 1) * C) >> (l + 1), ((i + 1) * C) >> l
-                pl, pr = _pop(a, mid, d), _pop(mid, b, d)
-                node = (1 << l) + i
-                if pl == 0:
-                    x = 0
-                elif pr == 0:
-                    x = m
-                elif m <= _SEQ_MAX:
-                    x = seq_draw(_mix64(tk ^ ((0x9E3779B97F4A7C15 * node) & _M64)), pl + pr, pl, m)
-                else:
-                    x = hyper_draw(pl + pr, pl, m, _uniform53(tk, node))
-            nxt[2 * i], nxt[2 * i + 1] = x, m - x
-        cur = nxt
-    cnt = np.zeros(C, dtype=np.int64)
-    for i in range(1 << L):
-        a = (i * C) >> L
-        if ((i + 1) * C) >> L == a + 1:
-            cnt[a] = cur[i]
-    return cnt
+    v = row_perm(ck, d, np.arange(k, dtype=np.uint64))
+    return np.bincount((v >> np.uint64(12)).astype(np.int64), minlength=C).astype(np.int64)
 
 
 def chunk_perm(ckey, c, clen, t):
