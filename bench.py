@@ -363,6 +363,7 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--step-times", action="store_true", help="per-step times (HIP events) on stderr")
     ap.add_argument("--row-groups", type=int, default=None,
                     help="sparse QSGD / TopK execution hint: fold row group g while group g+1 is filtered")
     ap.add_argument("--compat", action="store_true",
@@ -525,12 +526,20 @@ def main():
         _lib.profile_collect(kname)             # drop anything recorded before the timed region
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if args.step_times:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        evs[0].record()
+    for i in range(args.steps):
         step()
+        if args.step_times:
+            evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.step_times and rank == 0:
+        print(json.dumps({"step_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(args.steps)]}),
+              file=sys.stderr)
     _lib.profile_enable(False)
     kms, klaunch = _lib.profile_collect(wl["kernel"])
     others = {}
@@ -561,11 +570,32 @@ def main():
         # gather's physical floor is the expected number of distinct lines touched, x 128 B
         nr = len(range(specs.index("randk:1%"), n, len(specs))) if mixed else n
         line_floor = nr * (d / 32.0) * (1.0 - (1.0 - k / d) ** 32) * 128 + (4 * d if wl["kernel"] == "k_randk_fold" else 0)
+    randk_group = None
+    if mixed and "randk:1%" in specs:
+        # C5's RandK group: counts + list-free fold; algorithmic 4 N_r K + 4 D, the 128-B line floor
+        # of its gathers, and the PMC traffic of the fold (profiles/pmc_c5_randk.json)
+        nr = len(range(specs.index("randk:1%"), n, len(specs)))
+        rk_ms = sum(others.get(kk, 0.0) for kk in ("k_randk_counts", "k_randk_fold"))
+        rk_floor = nr * (d / 32.0) * (1.0 - (1.0 - k / d) ** 32) * 128 + 4 * d
+        rk_traffic = None
+        pmc_rk = os.path.join(ROOT, "profiles", "pmc_c5_randk.json")
+        if os.path.exists(pmc_rk):
+            with open(pmc_rk) as f:
+                rk_traffic = json.load(f).get("hbm_bytes_per_launch")
+        if rk_ms:
+            randk_group = {"rows": nr, "ms_per_step": round(rk_ms, 4),
+                           "algorithmic_GBps": round((4 * nr * k + 4 * d) / (rk_ms * 1e-3) / 1e9, 1),
+                           "line_floor_bytes": int(rk_floor),
+                           "line_floor_GBps": round(rk_floor / (rk_ms * 1e-3) / 1e9, 1),
+                           "fold_traffic_bytes": rk_traffic}
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            pj = json.load(f)
+        # only the PMC pass of this line's dominant kernel (compat lines run another kernel)
+        if wl["kernel"] in pj.get("kernel", ""):
+            traffic = pj.get("hbm_bytes_per_launch")
 
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d, n_total if strong else n * world,
@@ -612,6 +642,8 @@ def main():
                             if line_floor else {})},
             "cpu_baseline": cpu,
         }
+        if randk_group:
+            line["randk_group"] = randk_group
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -24,17 +24,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL_SUBSTR = {"c3": "k_topk_filter_fast", "c4": "k_ds_filter", "reduce": "k_reduce_vec",
-                 "c2": "k_randk_coarse", "c5": "k_ds_filter"}
+                 "c2": "k_randk_gen", "c5": "k_ds_filter"}
 
 
-def run_pass(ctr, wl, extra, outdir):
+def run_pass(ctr, wl, extra, outdir, kernel):
     cmd = ["rocprofv3", "--pmc", ctr, "-d", outdir, "-o", "run", "--output-format", "csv", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--no-cpu-baseline"] + extra
     subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL, timeout=600)
     vals, disp = collections.defaultdict(float), set()
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL_SUBSTR[wl] in r["Kernel_Name"]:
+            if kernel in r["Kernel_Name"]:
                 vals[r["Counter_Name"]] += float(r["Counter_Value"])
                 disp.add(r.get("Dispatch_Id") or r.get("Correlation_Id"))
     return vals[ctr], len(disp)
@@ -45,20 +45,24 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--kernel", default=None, help="another kernel of the workload (default: its dominant one)")
+    ap.add_argument("--tag", default=None, help="output name profiles/pmc_<tag>.json (default: the workload)")
     a = ap.parse_args()
+    kernel = a.kernel or KERNEL_SUBSTR[a.workload]
+    tag = a.tag or a.workload
     extra = ["--steps", str(a.steps), "--warmup", "1"] + (["--n", str(a.n)] if a.n else [])
     os.environ.setdefault("TMPDIR", "/tmp")
-    base = os.path.join(ROOT, "gpurun_out", f"pmc_traffic_{a.workload}")
-    fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch")
-    write, nw = run_pass("WRITE_SIZE", a.workload, extra, base + "_write")
+    base = os.path.join(ROOT, "gpurun_out", f"pmc_traffic_{tag}")
+    fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch", kernel)
+    write, nw = run_pass("WRITE_SIZE", a.workload, extra, base + "_write", kernel)
     launches = max(nf, nw, 1)
-    res = {"workload": a.workload, "kernel": KERNEL_SUBSTR[a.workload], "n_override": a.n,
+    res = {"workload": a.workload, "kernel": kernel, "n_override": a.n,
            "launches": launches, "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024 / launches),
            "correction": "2 x FETCH_SIZE (gfx950 counts half of 16 B/lane streaming reads) + WRITE_SIZE, KiB->B"}
     for d in ("profiles", "gpurun_out"):       # gpurun_out/ is what travels back from the GPU box
         os.makedirs(os.path.join(ROOT, d), exist_ok=True)
-        with open(os.path.join(ROOT, d, f"pmc_{a.workload}.json"), "w") as f:
+        with open(os.path.join(ROOT, d, f"pmc_{tag}.json"), "w") as f:
             json.dump(res, f, indent=1)
     print(json.dumps(res))
 
