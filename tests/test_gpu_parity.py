@@ -533,3 +533,33 @@ def test_signed_zero_in_sparse_fold(ag, spec, n, weights):
     # the pointer-array entry point and the wire path (sparse payloads) give the same bits
     rt = torch.from_numpy(rows).cuda()
     assert_bitexact(red([rt[i].clone() for i in range(n)], weights=w, **kw), want)
+
+
+def test_weighted_fold_vs_reference(ag):
+    """The fold with client weights != 1 against the reference's own DCGD / FedAvg serverGradient
+    (tests/golden/weighted.*, make_golden_weighted.py): both entry points and the protocol body
+    with a host params_current, bit-exact."""
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(gold, "weighted.json")))
+    arr = np.load(os.path.join(gold, "weighted.npz"))
+    for m in meta:
+        c = m["case"]
+        x, rows, w = arr[f"c{c}_x"], arr[f"c{c}_rows"], m["weights"]
+        want = arr[f"c{c}_{m['algorithm']}_gs"]
+        xt, rt = torch.from_numpy(x).cuda(), torch.from_numpy(rows).cuda()
+        assert_bitexact(ag.reduce_rows(xt, rt, w), want)
+        assert_bitexact(ag.reduce_rows(xt, [rt[i] for i in range(len(w))], w), want)
+
+        class Buf:
+            def waitForItem(self):
+                pass
+
+            def get(self, i, _r=rows, _w=w):
+                return {"model": torch.from_numpy(_r[i].copy()), "client_state": {"weight": _w[i]}}
+        H = {"fl_dtype": torch.float32, "compressor_master": ag.initCompressor("ident", x.size)}
+        body = ag.serverGradientMaster if m["algorithm"] == "dcgd" else ag.serverGradientPlain
+        got = body(Buf(), len(w), None, torch.from_numpy(x.copy()), H)
+        assert got.device.type == "cpu"
+        assert_bitexact(got, want)

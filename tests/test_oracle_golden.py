@@ -258,3 +258,24 @@ def test_dithering_closed_form_equals_loop(spec):
             loop[c12 & ~c3] = lv[s + 1]
         fast = oc.dither_levels(y, u, lv)
     np.testing.assert_array_equal(fast.view(np.uint32), loop.view(np.uint32))
+
+
+def _weighted():
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(gold, "weighted.json")))
+    arr = np.load(os.path.join(gold, "weighted.npz"))
+    return meta, arr
+
+
+def test_oracle_weighted_fold_vs_reference():
+    """The oracle's fold with Python-float weights != 1 (w * (x - x_i) in fp32, Python-float total
+    as the divisor) equals the reference's DCGD / FedAvg serverGradient on the same inputs."""
+    meta, arr = _weighted()
+    for m in meta:
+        c = m["case"]
+        x, rows = arr[f"c{c}_x"], arr[f"c{c}_rows"]
+        got = oc.server_gradient(x, list(rows), m["weights"])
+        want = arr[f"c{c}_{m['algorithm']}_gs"]
+        assert np.array_equal(np.asarray(got, np.float32).view(np.uint32), want.view(np.uint32)), m
