@@ -223,6 +223,10 @@ extern "C" int flc_unpack_reduce(const flc_codec_params* prm, const void* d_payl
                                  float w_total, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
     if (!prm || !known(prm->codec)) { set_error("flc_unpack_reduce: unknown codec"); return FLC_ERR_UNSUPPORTED; }
     if (n < 0 || d < 0 || (d > 0 && !d_out)) { set_error("flc_unpack_reduce: bad n/d/out"); return FLC_ERR_ARG; }
+    if (n > FLC_MAX_ROWS) {
+        set_error("flc_unpack_reduce: n=%lld payloads, at most %d per call", (long long)n, FLC_MAX_ROWS);
+        return FLC_ERR_UNSUPPORTED;
+    }
     if (n > 0 && d > 0 && !d_payloads && !d_payload_ptrs) { set_error("flc_unpack_reduce: no payloads"); return FLC_ERR_ARG; }
     if (d_payloads && ld_bytes < payload_bytes(prm, d)) { set_error("flc_unpack_reduce: ld_bytes < payload size"); return FLC_ERR_ARG; }
     return unpack_reduce_run(prm, (const char*)d_payloads, ld_bytes, (const char* const*)d_payload_ptrs, n, d, d_w,
@@ -234,6 +238,11 @@ extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern*
                                  float* d_pnorms_out, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
     if (!prm || !known(prm->codec)) { set_error("flc_encode_reduce: unknown codec"); return FLC_ERR_UNSUPPORTED; }
     if (n < 0 || d < 0 || (d > 0 && !d_out)) { set_error("flc_encode_reduce: bad n/d/out"); return FLC_ERR_ARG; }
+    if (n > FLC_MAX_ROWS) {   // per-row kernels index rows by blockIdx.y
+        set_error("flc_encode_reduce: n=%lld rows, at most %d per call (fold larger rounds as partials)", (long long)n,
+                  FLC_MAX_ROWS);
+        return FLC_ERR_UNSUPPORTED;
+    }
     if (n > 0 && d > 0 && !d_rows && !d_row_ptrs) { set_error("flc_encode_reduce: no rows"); return FLC_ERR_ARG; }
     if (d_rows && ld < d) { set_error("flc_encode_reduce: ld < d"); return FLC_ERR_ARG; }
     hipStream_t st = (hipStream_t)stream;

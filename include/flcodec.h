@@ -132,6 +132,10 @@ int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, const float*
                const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws,
                size_t ws_bytes, void* stream);
 
+/* Rows per flc_encode_reduce / flc_unpack_reduce call (larger rounds: fold the row blocks as
+ * partials with w_total = 1 and combine them, as the multi-GPU path does). */
+#define FLC_MAX_ROWS 65535
+
 /* ----------------------------------------------------------------------------------------
  * Fused batch encode + reduce — the simulated uplink of one round in one call:
  *     out = (sum_i w_i * C_i(row_i)) / w_total
