@@ -360,8 +360,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--n", type=int, default=None, help="override clients per GPU")
-    ap.add_argument("--d", type=int, default=None, help="override D")
+    # --clients / --dim: the spellings to use under torch.distributed.run (its parser takes "--n" as an
+    # ambiguous abbreviation of its own options)
+    ap.add_argument("--n", "--clients", dest="n", type=int, default=None, help="override clients per GPU")
+    ap.add_argument("--d", "--dim", dest="d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--step-times", action="store_true", help="per-step times (HIP events) on stderr")
     ap.add_argument("--row-groups", type=int, default=None,
@@ -399,13 +401,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # rehearsal of the multi-rank path on a one-GPU box (never the measured configuration):
+    # FLC_BENCH_SHARE_GPU=1 puts every rank on cuda:0, FLC_BENCH_BACKEND=gloo swaps RCCL for gloo
+    if os.environ.get("FLC_BENCH_SHARE_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         # one node (the bench contract): RCCL's bootstrap on loopback unless the caller chose
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("FLC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from flpytorch_amd import _lib
     from flpytorch_amd import aggregation as ag
