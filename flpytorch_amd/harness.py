@@ -152,7 +152,7 @@ class Simulation:
 
     def __init__(self, algorithm, client_compressor, model, x0, num_clients, clients_per_round, rounds,
                  local_lr, global_lr, local_iters=1, runtime_seed=0, device="cuda", sampling="uniform",
-                 poisson_p=None, init_compressor=None, server_gradient=None, record_iterates=False):
+                 poisson_p=None, init_compressor=None, server_gradient=None, record_iterates=False, wire=False):
         algorithm = algorithm.lower()
         if algorithm not in ("dcgd", "fedavg"):
             raise ValueError(f"harness drives dcgd / fedavg, not {algorithm!r}")  # algorithms.py:1954 style
@@ -165,6 +165,12 @@ class Simulation:
         self.num_clients, self.per_round, self.rounds = int(num_clients), int(clients_per_round), int(rounds)
         self.local_lr, self.global_lr, self.local_iters = float(local_lr), float(global_lr), int(local_iters)
         self.record_iterates = record_iterates
+        # wire=True (DCGD): each client's compressed gradient crosses the "network" as the wire
+        # message (Compressor.compressPayload, include/flcodec.h layouts) and the server side
+        # rebuilds it (decompressPayload, bit-exact) before the local step it applies — the
+        # physical form of last_need_to_send_advance (the reference pickles dense tensors,
+        # comm_socket.py:16-82); bytes per client in client_state["stats"]["payload_bytes"]
+        self.wire = bool(wire)
         self.iterates = []                                                       # x after each round (opt-in)
         self.init_compressor = init_compressor or ag.initCompressor
         # DCGD folds then applies the master (identity) compressor (algorithms.py:1748-1770);
@@ -205,7 +211,12 @@ class Simulation:
             f, g = self.model.value_and_gradient(xi, client_id)
             if self.algorithm == "dcgd":                                         # algorithms.py:1741-1745
                 comp = cs["client_compressor"]
-                c = comp.compressVector(g)
+                if self.wire:
+                    msg = comp.compressPayload(g)
+                    cs["stats"]["payload_bytes"] = cs["stats"].get("payload_bytes", 0) + msg.numel()
+                    c = comp.decompressPayload(msg, g.numel())
+                else:
+                    c = comp.compressVector(g)
                 cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
             else:                                                                # algorithms.py:1803-1807
                 c = g

@@ -72,3 +72,21 @@ def test_harness_patterns_are_the_reference_draws(ag):
     assert len(drawn) == len(want)
     for a, b in zip(drawn, want):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] == "dcgd"])
+def test_harness_wire_mode_same_round(ag, name):
+    """wire=True: every client's compressed gradient travels as its wire message
+    (compressPayload -> decompressPayload) — the round is bit-identical to the in-memory one and
+    matches the reference run; the bytes each client ships are recorded."""
+    base = simulation(name, "cuda", record_iterates=True)
+    base.run()
+    sim = simulation(name, "cuda", record_iterates=True, wire=True)
+    H = sim.run()
+    check_history(name, H, rel=1e-6)
+    for a, b in zip(base.iterates, sim.iterates):
+        assert np.array_equal(a.numpy().view(np.uint32), b.numpy().view(np.uint32))
+    per_msg = ag.initCompressor(META[name]["client_compressor"], META[name]["D"]).payloadBytes()
+    for r in H["history"].values():
+        for st in r["client_states"].values():
+            assert st["client_state"]["stats"]["payload_bytes"] == per_msg * META[name]["local_iters"]
