@@ -309,6 +309,60 @@ def e2e_wire(args):
                       "note": "payloads in pinned host memory; 2-stream H2D/fold overlap, blocks of 8 clients"}))
 
 
+def shift(args):
+    """The compressed algorithms' client step on one client row, fused in one
+    call (Compressor.compressShift -> flc_encode_shift) against the same step as the reference
+    writes it in torch on the GPU (compressVector(a - b), then the scalar ops):
+      diana   m = C(g - h); h' = h + alpha m                    algorithms.py:1383-1391
+      ef21    g' = g_prev + C(g - g_prev) * mult                algorithms.py:1506-1517
+      marina  g' = g_prev + C(g_cur - g_prev_x)                 algorithms.py:537
+    Device-RNG draws.  Bytes of the fused step: a, b read, msg written (+ h read and written for
+    diana, + base read for ef21 / marina).  Own line, not `value`."""
+    from flpytorch_amd import aggregation as ag
+    wl = dict(WORKLOADS[args.workload])
+    d = args.d or wl["d"]
+    spec = wl["spec"] if wl["spec"] != "mixed" else "qsgd:127"
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device=dev).manual_seed(11)
+    a = torch.randn(d, generator=g, device=dev)
+    b = torch.randn(d, generator=g, device=dev) * 0.5
+    base = torch.randn(d, generator=g, device=dev)
+    c = ag.initCompressor(spec, d)
+    c.device_rng = (20241015, 3)
+    alpha = 1.0 / (1.0 + c.getW()) if c.isUnbiasedCompressor() else 1.0
+    msg_out = torch.empty(d, device=dev)
+    h_out = torch.empty(d, device=dev)
+    algo = args.shift
+    if algo == "diana":
+        fused = lambda: c.compressShift(a, b, alpha=alpha, shift=b, shift_out=h_out, out=msg_out)
+        torch_step = lambda: (lambda m: (m, b + alpha * m))(c.compressVector(a - b))
+        moved = 4 * d * 5                     # a, b (= h) read; msg, h' written; h read for the update
+    elif algo == "ef21":
+        fused = lambda: c.compressShift(a, b, scale=alpha, base=b, out=msg_out)
+        torch_step = lambda: b + c.compressVector(a - b) * alpha
+        moved = 4 * d * 3
+    else:
+        fused = lambda: c.compressShift(a, b, base=base, out=msg_out)
+        torch_step = lambda: base + c.compressVector(a - b)
+        moved = 4 * d * 4
+    res = {}
+    for name, fn in (("fused_flc_encode_shift", fused), ("torch_ops_around_compressVector", torch_step)):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = round((time.perf_counter() - t0) / args.steps * 1e3, 4)
+    print(json.dumps({"mode": f"{algo} client step (compressShift) vs the reference's torch expression on the GPU",
+                      "codec": spec, "D": d, "ms_per_step": res,
+                      "fused_GBps": round(moved / (res["fused_flc_encode_shift"] * 1e-3) / 1e9, 1),
+                      "bytes_per_step": moved,
+                      "note": "device-RNG draws; bytes: the step's vectors read / written once (dithering adds a norm pass)"}))
+
+
 def dropin(args):
     """The drop-in path as the reference's algorithms drive it after install(): every client's
     Compressor.compressVector (generateCompressPattern on the caller's numpy stream first: compat
@@ -365,6 +419,8 @@ def main():
     ap.add_argument("--n", "--clients", dest="n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", "--dim", dest="d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shift", choices=["diana", "ef21", "marina"], default=None,
+                    help="the compressed algorithms' client step on one row (flc_encode_shift) vs torch ops")
     ap.add_argument("--step-times", action="store_true", help="per-step times (HIP events) on stderr")
     ap.add_argument("--row-groups", type=int, default=None,
                     help="sparse QSGD / TopK execution hint: fold row group g while group g+1 is filtered")
@@ -382,6 +438,8 @@ def main():
                     help="end-to-end: client rows start in pinned host memory, the [D] result lands in host memory "
                          "(H2D + encode+reduce + D2H per step; PCIe-bound; reported in DESIGN.md, never as value)")
     args = ap.parse_args()
+    if args.shift:
+        return shift(args)
     if args.dropin:
         return dropin(args)
     if args.e2e and args.wire:
