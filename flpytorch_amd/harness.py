@@ -26,9 +26,22 @@ model-side local gradient (out of the hot path) on the device
 ``device="cpu"`` mirrors the reference's ``--gpu -1`` runs (config C1: client rows cross to the
 GPU for the codec and the fold and back), ``device="cuda"`` keeps the whole round on the MI355X.
 
-Only the algorithms whose client step is the plain ``C(g)`` (DCGD) or ``g`` (FedAvg, FedProx
-without its proximal term is not included) are driven here; the others' serverGradient bodies are
-covered by ``aggregation.install``.
+Algorithms driven here: DCGD (client step ``C(g)``), FedAvg (``g``), and the shifted ones whose
+client step is the fused shift codec (``Compressor.compressShift``, one flc_encode_shift pass):
+
+  DIANA   algorithms.py:1317-1428  h0 = h = 0 or the full gradient at x0 (get_initial_shift,
+                                   474-479; run.py:408-418), alpha = 1 / (1 + w); client i keeps
+                                   h_i across rounds (findRecentRecordAndRemoveFromHistory,
+                                   371-399); step m_i = C(g - h_i), h_i += alpha m_i (dianaStep);
+                                   server: gs = fold, H['m'] = gs, returns h + gs, then
+                                   h += alpha m
+  EF21    algorithms.py:1432-1554  round 0 samples every client (request_use_full_list_of_clients,
+                                   model_funcs.py:470-475); a client's first step sends g and keeps
+                                   it as g_i; later g_i += C(g - g_i) * mult (ef21Step, mult =
+                                   1 / (1 + w) unless C is a contraction); server: fold + master
+                                   (identity) compressor
+
+The others' serverGradient bodies are covered by ``aggregation.install``.
 """
 import math
 
@@ -82,16 +95,20 @@ class DenseModel:
         self._dev = {}
 
     def _client_data(self, client, device):
-        key = (str(device), int(client))
+        key = (str(device), None if client is None else int(client))
         if key not in self._dev:
-            lo = int(client) * self.spc
-            self._dev[key] = (self.data[lo:lo + self.spc].to(device), self.targets[lo:lo + self.spc].to(device))
+            if client is None:                                  # set_client(None): the whole train set
+                self._dev[key] = (self.data.to(device), self.targets.to(device))  # (artificial_dataset.py:156-158)
+            else:
+                lo = int(client) * self.spc
+                self._dev[key] = (self.data[lo:lo + self.spc].to(device),
+                                  self.targets[lo:lo + self.spc].to(device))
         return self._dev[key]
 
     def value_and_gradient(self, x, client):
         """(f, g): the client's loss at x as a Python float (evaluateGradient's
         function_value.item(), algorithms.py:112) and its gradient as a flat [D] fp32 tensor on
-        x's device (mutils.get_gradient)."""
+        x's device (mutils.get_gradient).  ``client=None``: the whole train set (run.py:408-413)."""
         params, off = [], 0
         for s in self.shapes:
             n = math.prod(s)
@@ -143,19 +160,54 @@ class _Buffer:
         return len(self.items)
 
 
-class Simulation:
-    """One experiment: ``rounds`` communication rounds of ``algorithm`` ("dcgd" | "fedavg") with
-    the client codec ``client_compressor`` (the reference's spec grammar), starting at ``x0``.
+def find_recent_and_remove(H, client_id, field):
+    """findRecentRecordAndRemoveFromHistory (algorithms.py:371-399): the newest round that sampled
+    the client holds the field (None after a previous read) or ends the search."""
+    for r in sorted(H["history"], reverse=True):
+        states = H["history"][r]["client_states"]
+        if client_id in states:
+            st = states[client_id]["client_state"]
+            if field in st:
+                v, st[field] = st[field], None
+                return v
+            return None
+    return None
 
-    ``init_compressor`` / ``server_gradient`` default to the product (flpytorch_amd.aggregation:
-    HIP codecs, HIP fold); tests may pass other implementations of the same protocol."""
+
+def _on_gpu(step):
+    """Run a shift-codec client step on the MI355X whatever device the client state lives on
+    (``device="cpu"``: the --gpu -1 layout, tensors cross to the GPU and back like the DCGD codec)."""
+    def run(comp, *tensors, **kw):
+        home = tensors[0].device
+        if home.type == "cuda":
+            return step(comp, *tensors, **kw)
+        out = step(comp, *[t.cuda() if torch.is_tensor(t) else t for t in tensors], **kw)
+        return tuple(o.to(home) for o in out) if isinstance(out, tuple) else out.to(home)
+    return run
+
+
+ALGORITHMS = ("dcgd", "fedavg", "diana", "ef21")
+
+
+class Simulation:
+    """One experiment: ``rounds`` communication rounds of ``algorithm`` (one of ``ALGORITHMS``)
+    with the client codec ``client_compressor`` (the reference's spec grammar), starting at ``x0``.
+
+    ``init_compressor`` / ``server_gradient`` / ``diana_step`` / ``ef21_step`` default to the
+    product (flpytorch_amd.aggregation: HIP codecs, HIP fold, fused shift codec); tests may pass
+    other implementations of the same protocol."""
 
     def __init__(self, algorithm, client_compressor, model, x0, num_clients, clients_per_round, rounds,
                  local_lr, global_lr, local_iters=1, runtime_seed=0, device="cuda", sampling="uniform",
-                 poisson_p=None, init_compressor=None, server_gradient=None, record_iterates=False, wire=False):
+                 poisson_p=None, init_compressor=None, server_gradient=None, record_iterates=False, wire=False,
+                 initialize_shifts_policy="zero", diana_step=None, ef21_step=None):
         algorithm = algorithm.lower()
-        if algorithm not in ("dcgd", "fedavg"):
-            raise ValueError(f"harness drives dcgd / fedavg, not {algorithm!r}")  # algorithms.py:1954 style
+        if algorithm not in ALGORITHMS:
+            raise ValueError(f"harness drives {', '.join(ALGORITHMS)}, not {algorithm!r}")  # algorithms.py:1954 style
+        if wire and algorithm != "dcgd":
+            raise ValueError("wire mode drives DCGD's compressVector messages only")
+        if initialize_shifts_policy not in ("zero", "full_gradient_at_start"):
+            raise ValueError(f"unknown initialize_shifts_policy {initialize_shifts_policy!r}")  # opts.py:437-441
         self.algorithm = algorithm
         self.spec = client_compressor.lower()                                    # opts.py:497 lowercases argv
         self.model = model
@@ -173,10 +225,13 @@ class Simulation:
         self.wire = bool(wire)
         self.iterates = []                                                       # x after each round (opt-in)
         self.init_compressor = init_compressor or ag.initCompressor
-        # DCGD folds then applies the master (identity) compressor (algorithms.py:1748-1770);
-        # FedAvg returns the fold (1810-1832)
-        self.server_gradient = server_gradient or (ag.serverGradientMaster if algorithm == "dcgd"
-                                                   else ag.serverGradientPlain)
+        self.diana_step = diana_step or _on_gpu(ag.dianaStep)
+        self.ef21_step = ef21_step or _on_gpu(ag.ef21Step)
+        # DCGD / EF21 fold then apply the master (identity) compressor (algorithms.py:1748-1770,
+        # 1521-1546); FedAvg returns the fold (1810-1832); DIANA returns h + fold (1395-1421)
+        default_fold = {"dcgd": ag.serverGradientMaster, "ef21": ag.serverGradientMaster,
+                        "fedavg": ag.serverGradientPlain, "diana": ag.serverGradientDIANA}[algorithm]
+        self.server_gradient = server_gradient or default_fold
         self.np_random = np.random.RandomState()
         self.np_random.seed(int(runtime_seed))                                   # run.py:343-345
         self.sampled = get_sampled_clients(self.num_clients, self.per_round, self.rounds, self.np_random,
@@ -191,43 +246,78 @@ class Simulation:
                 self.H["w"] = c.getW()
             elif c.isContractionCompressor():
                 self.H["alpha"] = c.getAlphaContraction()
+        elif algorithm == "diana":                                               # algorithms.py:1346-1357
+            w = self.init_compressor(self.spec, self.D).getW()
+            if initialize_shifts_policy == "full_gradient_at_start":             # run.py:408-413
+                _, h0 = self.model.value_and_gradient(self.x, None)
+            else:
+                h0 = torch.zeros(self.D, dtype=torch.float32, device=self.device)
+            self.H.update({"h0": h0.detach().clone(), "h": h0.detach().clone(), "alpha": 1.0 / (1.0 + w), "w": w})
+        elif algorithm == "ef21":                                                # algorithms.py:1460-1468
+            self.H["request_use_full_list_of_clients"] = True
 
-    # algorithms.clientState (2015-2069) with the class part of DCGD (1729-1732) / FedAvg (1793-1794)
+    # algorithms.clientState (2015-2069) with the class parts: DCGD 1729-1732, FedAvg 1793-1794,
+    # DIANA 1360-1373, EF21 1471-1484
     def client_state(self, client_id, rnd):
         cs = {}
-        if self.algorithm == "dcgd":
+        if self.algorithm in ("dcgd", "diana", "ef21"):
             comp = self.init_compressor(self.H["client_compressor"], self.D)
             comp.generateCompressPattern(self.np_random, str(self.device), client_id, self.H)
             cs["client_compressor"] = comp
+        if self.algorithm == "diana":
+            hi = find_recent_and_remove(self.H, client_id, "hi")
+            cs["hi"] = self.H["h0"].detach().clone() if hi is None else hi
+        elif self.algorithm == "ef21":
+            cs["g_prev"] = find_recent_and_remove(self.H, client_id, "g_prev")
         cs.update({"algorithm": self.algorithm, "client_id": client_id, "weight": 1.0, "round": rnd,
                    "approximate_f_value": [], "seed": self.np_random.randint(2 ** 31),
                    "stats": {"send_scalars_to_master": 0}})
         return cs
+
+    # the class's localGradientEvaluation after the gradient is known: the vector the local SGD
+    # step applies
+    def client_step(self, cs, g):
+        comp = cs.get("client_compressor")
+        if self.algorithm == "fedavg":                                           # algorithms.py:1803-1807
+            cs["stats"]["send_scalars_to_master"] += g.numel()
+            return g
+        if self.algorithm == "dcgd":                                             # algorithms.py:1741-1745
+            if self.wire:
+                msg = comp.compressPayload(g)
+                cs["stats"]["payload_bytes"] = cs["stats"].get("payload_bytes", 0) + msg.numel()
+                c = comp.decompressPayload(msg, g.numel())
+            else:
+                c = comp.compressVector(g)
+            cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
+            return c
+        if self.algorithm == "diana":                                            # algorithms.py:1383-1392
+            m, cs["hi"] = self.diana_step(comp, g, cs["hi"], self.H["alpha"])
+            cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
+            return m
+        if cs["g_prev"] is None:                                                 # EF21, algorithms.py:1494-1500
+            cs["g_prev"] = g                                                     # (first step: not counted)
+            return g
+        g_next = self.ef21_step(comp, g, cs["g_prev"])                           # algorithms.py:1502-1518
+        cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
+        cs["g_prev"] = g_next
+        return g_next
 
     # local_training (model_funcs.py:318-388) + train_model's loop (617-723)
     def local_training(self, cs, client_id):
         xi = self.x.clone()
         for _ in range(self.local_iters):
             f, g = self.model.value_and_gradient(xi, client_id)
-            if self.algorithm == "dcgd":                                         # algorithms.py:1741-1745
-                comp = cs["client_compressor"]
-                if self.wire:
-                    msg = comp.compressPayload(g)
-                    cs["stats"]["payload_bytes"] = cs["stats"].get("payload_bytes", 0) + msg.numel()
-                    c = comp.decompressPayload(msg, g.numel())
-                else:
-                    c = comp.compressVector(g)
-                cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
-            else:                                                                # algorithms.py:1803-1807
-                c = g
-                cs["stats"]["send_scalars_to_master"] += g.numel()
+            c = self.client_step(cs, g)
             cs["approximate_f_value"].append(f)
             xi.add_(c.to(xi.device), alpha=-self.local_lr)                      # SGD step, momentum 0
         return {"model": xi, "client_id": client_id, "client_state": cs}
 
     # run_one_communication_round (model_funcs.py:459-614)
     def run_round(self, rnd):
-        clients = self.sampled[rnd]
+        if self.H.get("request_use_full_list_of_clients"):                       # model_funcs.py:470-475
+            clients = np.arange(self.H["total_clients"])
+        else:
+            clients = self.sampled[rnd]
         buf = _Buffer()
         for cid in clients:
             cs = self.client_state(int(cid), rnd)
@@ -245,8 +335,8 @@ class Simulation:
         states = {}
         for item in buf.items:
             fvalues += item["client_state"]["approximate_f_value"]
-            st = dict(item["client_state"])
-            st.pop("client_compressor", None)
+            st = item["client_state"]
+            st.pop("client_compressor", None)                                    # algorithms.py:2198-2199
             states[item["client_id"]] = {"client_state": st}
         self.H["history"][rnd] = {
             "client_states": states,
@@ -254,6 +344,12 @@ class Simulation:
             "approximate_f_avg_value": float(np.mean(fvalues)) if fvalues else float("nan"),
             "x_before_round": l2_norm_of_vec(x_prev),
         }
+        # the class's serverGlobalStateUpdate (2239-2240)
+        if self.algorithm == "diana":                                            # algorithms.py:1424-1428
+            self.H["h"] = self.H["h"] + self.H["alpha"] * self.H["m"]
+        elif self.algorithm == "ef21":                                           # algorithms.py:1549-1554
+            self.H["compressor_master"].generateCompressPattern(self.np_random, str(self.device), -1, self.H)
+            self.H["request_use_full_list_of_clients"] = False
         return self.H["history"][rnd]
 
     def run(self):

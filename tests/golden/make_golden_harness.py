@@ -20,7 +20,10 @@ replay a run without the reference:
   (algorithms.py:2218-2223).
 
 Runs: the four of make_golden.py (C1 = FedAvg + ident; DCGD with randk / qsgd / topk) plus
-partial participation (2 of 4 clients per round) with 2 local steps, for DCGD randk and FedAvg.
+partial participation (2 of 4 clients per round) with 2 local steps, for DCGD randk and FedAvg;
+DIANA (randk / qsgd, zero and full-gradient initial shifts) and EF21 (topk = contraction, randk =
+unbiased: the 1 / (1 + w) multiplier) over enough rounds that clients come back to their stored
+shifts.  For DIANA the server shift h after every round's serverGlobalStateUpdate is recorded too.
 """
 import json
 import os
@@ -39,6 +42,14 @@ RUNS.update({
                             "--num-clients-per-round", "2", "-li", "2", "--rounds", "4"],
     "fedavg_p2_li2": ["--algorithm", "fedavg", "--client-compressor", "ident",
                       "--num-clients-per-round", "2", "-li", "2", "--rounds", "4"],
+    "diana_randk10_p2_li2": ["--algorithm", "diana", "--client-compressor", "randk:10%",
+                             "--num-clients-per-round", "2", "-li", "2", "--rounds", "5"],
+    "diana_qsgd10_fullgrad": ["--algorithm", "diana", "--client-compressor", "qsgd:10",
+                              "--initialize-shifts-policy", "full_gradient_at_start", "--rounds", "3"],
+    "ef21_topk10_p2_li2": ["--algorithm", "ef21", "--client-compressor", "topk:10%",
+                           "--num-clients-per-round", "2", "-li", "2", "--rounds", "5"],
+    "ef21_randk10_p2": ["--algorithm", "ef21", "--client-compressor", "randk:10%",
+                        "--num-clients-per-round", "2", "--rounds", "5"],
 })
 
 
@@ -60,12 +71,15 @@ def main():
 
     # the iterate after every round's global step (the model holds it when serverGlobalStateUpdate
     # runs, model_funcs.py:605-607); x0 from the start hook (run.py prunes tensors from H at the end)
-    iterates, starts = [], []
+    iterates, starts, shifts = [], [], []
     orig_sgsu = algorithms.serverGlobalStateUpdate
 
     def sgsu_wrap(clients_responses, model, *a, **k):
         iterates.append(mutils.get_params(model).detach().cpu().numpy().copy())
-        return orig_sgsu(clients_responses, model, *a, **k)
+        Hn = orig_sgsu(clients_responses, model, *a, **k)
+        if Hn["algorithm"] == "diana":
+            shifts.append(Hn["h"].detach().cpu().numpy().copy())         # h after h += alpha m
+        return Hn
     algorithms.serverGlobalStateUpdate = sgsu_wrap
     execution_context.simulation_start_fn = lambda H: starts.append(H["x0"].detach().cpu().numpy().copy())
 
@@ -83,6 +97,7 @@ def main():
         captured.clear()
         iterates.clear()
         starts.clear()
+        shifts.clear()
         result = {}
         execution_context.simulation_finish_fn = lambda H, _r=result: _r.update(H=H)
         refrun.runSimulation(mg.COMMON + extra + ["--run-id", name])
@@ -93,6 +108,8 @@ def main():
         arrays["data_A"], arrays["data_B"] = A, B
         arrays[f"{name}_x0"] = starts[0]
         arrays[f"{name}_iterates"] = np.stack(iterates)            # x after each round's global step
+        if shifts:
+            arrays[f"{name}_server_shift"] = np.stack(shifts)
         hist = H["history"]
         rounds = []
         for r in sorted(hist):
@@ -115,6 +132,7 @@ def main():
             "local_lr": float(args.local_lr), "global_lr": float(args.global_lr),
             "manual_runtime_seed": int(args.manual_runtime_seed), "samples_per_client": int(S),
             "D": int(H["D"]), "history": rounds,
+            "initialize_shifts_policy": args.initialize_shifts_policy,
         }
         print(name, [r["grad_sgd_server_l2"] for r in rounds])
     np.savez_compressed(os.path.join(HERE, "harness.npz"), **arrays)

@@ -16,7 +16,17 @@ def simulation(name, device, **kw):
     assert model.D == m["D"]
     return harness.Simulation(m["algorithm"], m["client_compressor"], model, DATA[f"{name}_x0"], m["num_clients"],
                               m["clients_per_round"], m["rounds"], m["local_lr"], m["global_lr"],
-                              local_iters=m["local_iters"], runtime_seed=m["manual_runtime_seed"], device=device, **kw)
+                              local_iters=m["local_iters"], runtime_seed=m["manual_runtime_seed"], device=device,
+                              initialize_shifts_policy=m.get("initialize_shifts_policy", "zero"), **kw)
+
+
+def check_server_shift(name, rounds_h, rtol=1e-5, atol=1e-7):
+    """DIANA: the server shift h after each round's serverGlobalStateUpdate (algorithms.py:1424-1428)
+    against the reference run's (``rounds_h``: the harness's h per round, collected by the test)."""
+    want = DATA[f"{name}_server_shift"]
+    assert len(rounds_h) == len(want)
+    for r, (got, w) in enumerate(zip(rounds_h, want)):
+        np.testing.assert_allclose(got, w, rtol=rtol, atol=atol, err_msg=f"{name} h after round {r}")
 
 
 def check_history(name, H, rel=1e-6):

@@ -1,8 +1,9 @@
 """The round harness on the product path (HIP codecs + HIP fold) against the reference's runs.
 
-Config C1 (FedAvg + ident, 4 clients, the "dense" MLP, D = 2465) and the DCGD runs (randk:10%,
-qsgd:10, topk:5%, plus partial participation with 2 local steps), captured from the real
-reference by tests/golden/make_golden_harness.py, replayed through flpytorch_amd.harness:
+Config C1 (FedAvg + ident, 4 clients, the "dense" MLP, D = 2465), the DCGD runs (randk:10%,
+qsgd:10, topk:5%, plus partial participation with 2 local steps) and the DIANA / EF21 runs (client
+steps on the fused shift codec), captured from the real reference by
+tests/golden/make_golden_harness.py, replayed through flpytorch_amd.harness:
   * device "cpu"  — the reference's --gpu -1 setting: the model side on the host, every codec call
     and the server fold in libflcodec.so (rows cross to the GPU and back);
   * device "cuda" — the whole round on the MI355X (the model side in torch on the GPU).
@@ -16,7 +17,7 @@ import pytest
 import torch
 
 from oracle import codecs as oc
-from tests.harness_cases import DATA, META, RUN_NAMES, check_history, simulation
+from tests.harness_cases import DATA, META, RUN_NAMES, check_history, check_server_shift, simulation
 
 pytestmark = pytest.mark.gpu
 
@@ -32,16 +33,25 @@ def ag():
 @pytest.mark.parametrize("name", RUN_NAMES)
 def test_harness_reproduces_reference_run(ag, name, device):
     folds = []
-    default_fold = ag.serverGradientMaster if META[name]["algorithm"] == "dcgd" else ag.serverGradientPlain
+    algo = META[name]["algorithm"]
+    default_fold = {"dcgd": ag.serverGradientMaster, "ef21": ag.serverGradientMaster,
+                    "fedavg": ag.serverGradientPlain, "diana": ag.serverGradientDIANA}[algo]
 
     def recording_fold(buf, clients, model, x, H):
         rows = [buf.get(i)["model"].detach().cpu().numpy().copy() for i in range(clients)]
         gs = default_fold(buf, clients, model, x, H)
-        folds.append((x.detach().cpu().numpy().copy(), rows, gs.detach().cpu().numpy().copy()))
+        fold = H["m"] if algo == "diana" else gs               # DIANA returns h + fold (algorithms.py:1419-1421)
+        folds.append((x.detach().cpu().numpy().copy(), rows, fold.detach().cpu().numpy().copy()))
         return gs
     sim = simulation(name, device, server_gradient=recording_fold, record_iterates=True)
-    H = sim.run()
-    check_history(name, H, rel=1e-6)
+    hs = []
+    for r in range(sim.rounds):
+        sim.run_round(r)
+        if algo == "diana":
+            hs.append(sim.H["h"].detach().cpu().numpy().copy())
+    check_history(name, sim.H, rel=1e-6)
+    if algo == "diana":
+        check_server_shift(name, hs)
     for r in range(META[name]["rounds"]):
         np.testing.assert_allclose(sim.iterates[r].numpy(), DATA[f"{name}_iterates"][r], rtol=1e-5, atol=1e-6,
                                    err_msg=f"{name} round {r}")
@@ -49,6 +59,36 @@ def test_harness_reproduces_reference_run(ag, name, device):
     for x, rows, gs in folds:
         want = oc.server_gradient(x, rows)
         assert np.array_equal(gs.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] in ("diana", "ef21")])
+def test_harness_shift_steps_run_fused_codec(ag, name):
+    """DIANA / EF21 client steps go through the fused shift codec (Compressor.compressShift ->
+    flc_encode_shift), and each step is bit-identical to the reference's torch expression on the
+    same inputs (algorithms.py:1386-1391, 1508-1513) evaluated with the product's compressVector."""
+    calls = []
+    orig = ag.Compressor.compressShift
+
+    def spy(self, a, b, **kw):
+        out = orig(self, a, b, **kw)
+        calls.append((self, a.clone(), b.clone(), kw, out))
+        return out
+    ag.Compressor.compressShift = spy
+    try:
+        sim = simulation(name, "cuda")
+        sim.run()
+    finally:
+        ag.Compressor.compressShift = orig
+    assert calls
+    for comp, a, b, kw, (msg, hout) in calls:
+        c = comp.compressVector(a - b)
+        if META[name]["algorithm"] == "diana":
+            want_h = kw["shift"] + kw["alpha"] * c
+            assert torch.equal(msg.view(torch.int32), c.view(torch.int32))
+            assert torch.equal(hout.view(torch.int32), want_h.view(torch.int32))
+        else:
+            want = kw["base"] + c * kw["scale"]
+            assert torch.equal(msg.view(torch.int32), want.view(torch.int32))
 
 
 def test_harness_patterns_are_the_reference_draws(ag):

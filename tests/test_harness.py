@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import codecs as oc
-from tests.harness_cases import DATA, META, RUN_NAMES, check_history, simulation
+from tests.harness_cases import DATA, META, RUN_NAMES, check_history, check_server_shift, simulation
 
 
 class OracleCompressorDouble:
@@ -52,12 +52,45 @@ def oracle_server_gradient(buf, clients, model, x, H):
     return torch.from_numpy(oc.server_gradient(x.cpu().numpy(), rows, w))
 
 
+def oracle_server_gradient_diana(buf, clients, model, x, H):
+    gs = oracle_server_gradient(buf, clients, model, x, H)
+    H["m"] = gs
+    return H["h"] + gs                                                   # algorithms.py:1419-1421
+
+
+def oracle_diana_step(comp, g, h, alpha):
+    m = comp.compressVector(g - h)                                       # algorithms.py:1386-1391
+    return m, h + alpha * m
+
+
+def oracle_ef21_step(comp, g, g_prev):
+    mult = 1.0 if comp.isContractionCompressor() else 1.0 / (1.0 + comp.getW())
+    return g_prev + comp.compressVector(g - g_prev) * mult               # algorithms.py:1508-1513
+
+
+def oracle_simulation(name, **kw):
+    fold = oracle_server_gradient_diana if META[name]["algorithm"] == "diana" else oracle_server_gradient
+    return simulation(name, "cpu", init_compressor=OracleCompressorDouble, server_gradient=fold,
+                      diana_step=oracle_diana_step, ef21_step=oracle_ef21_step, **kw)
+
+
+def run_collecting_shift(sim):
+    """sim.run(), keeping DIANA's server shift after every round."""
+    hs = []
+    for r in range(sim.rounds):
+        sim.run_round(r)
+        if "h" in sim.H:
+            hs.append(sim.H["h"].detach().cpu().numpy().copy())
+    return sim.H, hs
+
+
 @pytest.mark.parametrize("name", RUN_NAMES)
 def test_harness_replays_reference_runs(name):
-    sim = simulation(name, "cpu", init_compressor=OracleCompressorDouble, server_gradient=oracle_server_gradient,
-                     record_iterates=True)
-    H = sim.run()
+    sim = oracle_simulation(name, record_iterates=True)
+    H, hs = run_collecting_shift(sim)
     check_history(name, H)
+    if META[name]["algorithm"] == "diana":
+        check_server_shift(name, hs)
     # the iterate after every round's global step
     for r in range(META[name]["rounds"]):
         np.testing.assert_allclose(sim.iterates[r].numpy(), DATA[f"{name}_iterates"][r], rtol=1e-6, atol=1e-7,
@@ -101,4 +134,33 @@ def test_rejects_other_algorithms():
     from flpytorch_amd import harness
     m = harness.DenseModel(DATA["data_A"], DATA["data_B"], 16)
     with pytest.raises(ValueError):
-        harness.Simulation("diana", "ident", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu")
+        harness.Simulation("marina", "ident", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu")
+    with pytest.raises(ValueError):
+        harness.Simulation("diana", "randk:10%", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu",
+                           wire=True)
+    with pytest.raises(ValueError):
+        harness.Simulation("diana", "randk:10%", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu",
+                           initialize_shifts_policy="random")
+
+
+def test_find_recent_and_remove():
+    """findRecentRecordAndRemoveFromHistory (algorithms.py:371-399): newest round first, the field
+    is cleared once read, a round that sampled the client without the field ends the search."""
+    from flpytorch_amd.harness import find_recent_and_remove
+    H = {"history": {0: {"client_states": {1: {"client_state": {"hi": "a"}}, 2: {"client_state": {"hi": "b"}}}},
+                     1: {"client_states": {1: {"client_state": {"hi": "c"}}}},
+                     2: {"client_states": {2: {"client_state": {}}}}}}
+    assert find_recent_and_remove(H, 1, "hi") == "c"
+    assert H["history"][1]["client_states"][1]["client_state"]["hi"] is None
+    assert find_recent_and_remove(H, 1, "hi") is None
+    assert find_recent_and_remove(H, 2, "hi") is None          # round 2 sampled client 2 without "hi"
+    assert find_recent_and_remove(H, 3, "hi") is None
+
+
+def test_ef21_first_round_samples_every_client():
+    sim = oracle_simulation("ef21_randk10_p2")
+    sim.run_round(0)
+    assert list(sim.H["history"][0]["client_states"]) == list(range(META["ef21_randk10_p2"]["num_clients"]))
+    assert sim.H["request_use_full_list_of_clients"] is False
+    sim.run_round(1)
+    assert list(sim.H["history"][1]["client_states"]) == [int(c) for c in sim.sampled[1]]
