@@ -32,7 +32,7 @@ EXPORTS = [
     "flc_encode_workspace_size", "flc_encode",
     "flc_encode_reduce_workspace_size", "flc_encode_reduce",
     "flc_encode_shift_workspace_size", "flc_encode_shift",
-    "flc_payload_bytes", "flc_payload_format", "flc_pack_workspace_size", "flc_pack", "flc_unpack",
+    "flc_payload_bytes", "flc_payload_format", "flc_payload_validate", "flc_pack_workspace_size", "flc_pack", "flc_unpack",
     "flc_unpack_reduce_workspace_size", "flc_unpack_reduce",
     "flc_combine_workspace_size", "flc_combine_partials",
     "flc_combine_blocks_workspace_size", "flc_combine_blocks",
@@ -110,6 +110,7 @@ def load():
         lib.flc_payload_bytes.argtypes = [P(FlcCodecParams), i64]
         lib.flc_payload_bytes.restype = i64
         lib.flc_payload_format.argtypes = [P(FlcCodecParams)]
+        lib.flc_payload_validate.argtypes = [P(FlcCodecParams), vp, i64, i64]
         lib.flc_pack_workspace_size.argtypes = [P(FlcCodecParams), i64]
         lib.flc_pack_workspace_size.restype = sz
         lib.flc_pack.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, vp, sz, vp]

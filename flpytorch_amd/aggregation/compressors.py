@@ -372,15 +372,33 @@ class Compressor:
         return out.to("cpu") if host_in else out
 
     # -- wire format ------------------------------------------------------
-    def payloadBytes(self, d=None):
-        """Bytes of one row's payload (flc_payload_bytes: 16-B header + body, 16-B padded)."""
-        prm, _ = self.codec_params(torch.device("cpu")) if self.compressorType not in (
-            CompressorType.STANDARD_DITHERING_FP32, CompressorType.NATURAL_DITHERING_FP32) else (None, None)
-        if prm is None:
+    def _host_params(self):
+        """flc_codec_params without device resources (sizes, formats, host-side checks)."""
+        if self.compressorType in (CompressorType.STANDARD_DITHERING_FP32, CompressorType.NATURAL_DITHERING_FP32):
             prm = _lib.FlcCodecParams()
             prm.codec = int(self.compressorType)
             prm.s = int(self.s)
-        return int(_lib.load().flc_payload_bytes(ctypes.byref(prm), self._dim(d)))
+            return prm
+        return self.codec_params(torch.device("cpu"))[0]
+
+    def payloadBytes(self, d=None):
+        """Bytes of one row's payload (flc_payload_bytes: 16-B header + body, 16-B padded)."""
+        return int(_lib.load().flc_payload_bytes(ctypes.byref(self._host_params()), self._dim(d)))
+
+    def validatePayload(self, payload, d=None):
+        """Check a message received from a peer before it is decoded (flc_payload_validate, host
+        only): its size, header and codes fit this codec and d.  ``payload``: bytes-like, a uint8
+        numpy array or a host uint8 tensor.  Raises ValueError with the reason."""
+        if torch.is_tensor(payload):
+            if payload.dtype != torch.uint8 or payload.is_cuda:
+                raise TypeError("validatePayload: a host uint8 tensor (or bytes) is expected")
+            arr = payload.contiguous().numpy()
+        else:
+            arr = np.frombuffer(payload, dtype=np.uint8)
+        lib = _lib.load()
+        rc = lib.flc_payload_validate(ctypes.byref(self._host_params()), ctypes.c_void_p(arr.ctypes.data),
+                                      int(arr.nbytes), self._dim(d))
+        _lib.check(rc, "validatePayload")
 
     def _dim(self, d):
         if d is None:
@@ -422,6 +440,15 @@ class Compressor:
         d = self._dim(d)
         lib = _lib.load()
         prm, keep = self.codec_params(dev)
+        if payload.dtype != torch.uint8:
+            raise TypeError(f"decompressPayload: payload must be uint8 (got {payload.dtype})")
+        nbytes = int(lib.flc_payload_bytes(ctypes.byref(prm), d))
+        if payload.numel() < nbytes:
+            raise ValueError(f"decompressPayload: {payload.numel()} bytes, the payload of d={d} is {nbytes}")
+        # a host message (off the network) crosses to the device first; the kernel reads HBM only
+        payload = payload.reshape(-1)[:nbytes].to(device=dev)
+        if not payload.is_contiguous() or payload.data_ptr() % 16:
+            payload = payload.clone()
         out = torch.empty(d, dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
             rc = lib.flc_unpack(ctypes.byref(prm), ctypes.c_void_p(payload.data_ptr()), d,

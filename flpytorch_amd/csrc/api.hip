@@ -195,6 +195,12 @@ extern "C" int flc_payload_format(const flc_codec_params* prm) {
     return payload_format(prm);
 }
 
+extern "C" int flc_payload_validate(const flc_codec_params* prm, const void* h_payload, int64_t nbytes, int64_t d) {
+    if (!prm || !known(prm->codec)) { set_error("flc_payload_validate: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (d < 0 || nbytes < 0 || (nbytes > 0 && !h_payload)) { set_error("flc_payload_validate: bad payload/nbytes/d"); return FLC_ERR_ARG; }
+    return payload_validate(prm, (const uint8_t*)h_payload, nbytes, d);
+}
+
 extern "C" size_t flc_pack_workspace_size(const flc_codec_params* prm, int64_t d) {
     if (!prm || !known(prm->codec) || d < 0) return 0;
     return pack_workspace(prm, d);

@@ -135,6 +135,7 @@ int rk_unpack_reduce(const flc_codec_params* prm, const char* base, int64_t ld, 
                      int64_t d, const float* w, float wt, float* out, bool reduce, void* wsp, size_t ws_bytes,
                      hipStream_t st);
 int payload_format(const flc_codec_params* prm);
+int payload_validate(const flc_codec_params* prm, const uint8_t* p, int64_t nbytes, int64_t d);
 size_t pack_workspace(const flc_codec_params* prm, int64_t d);
 int pack_run(const flc_codec_params* prm, const flc_pattern* pat, const float* x, int64_t d, char* payload, void* ws,
              size_t ws_bytes, hipStream_t st);

@@ -3,7 +3,7 @@
 // 367-368 count these bits as last_need_to_send_advance, but the reference only ever moves the
 // dense decoded tensor; comm_socket.py pickles that).
 //
-// One row's payload: a 16-B header {u32 format, u32 count, f32 norm, u32 d} and a body, 16-B padded:
+// One row's payload: a 16-B header {u32 format, u32 count, f32 norm, u32 bad} and a body, 16-B padded:
 //   F32     ident / lazy / natural dithering (the reference's output is ~x): f32[d]
 //   Q8      standard dithering / QSGD / TernGrad, s <= 127: u8[d]   bit 7 sign, bits 0-6 level index
 //   Q16     standard dithering, 127 < s <= 32767:         u16[d]  bit 15 sign, bits 0-14 level index
@@ -23,6 +23,8 @@
 // (levels[i] * sign) * norm reproduces the element's bits (guess rint(y s), then its neighbours,
 // then a binary search); elements no level reproduces are counted in the header's `bad` field
 // (never seen: the encode's outputs are of that form by construction; the tests assert 0).
+#include <cstring>
+
 #include "wire_codes.hpp"
 
 namespace flc {
@@ -155,27 +157,32 @@ __global__ __launch_bounds__(256) void k_pack_write(const float* __restrict__ v,
 }
 
 // ---- unpack (one row) --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_unpack_dense(const char* __restrict__ payload, int64_t d,
+__global__ __launch_bounds__(256) void k_unpack_dense(const char* __restrict__ payload, int64_t d, int fmt, int s,
                                                       const float* __restrict__ levels, float* __restrict__ out) {
-    const PayloadHeader h = *reinterpret_cast<const PayloadHeader*>(payload);
+    // the format and level count come from the codec, never from the message: a header that lies
+    // cannot move a read past the body flc_payload_bytes sized (flc_payload_validate reports it)
+    const float norm = reinterpret_cast<const PayloadHeader*>(payload)->norm;
     const char* body = payload + 16;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
         float x;
-        if (h.fmt == FMT_F32) x = reinterpret_cast<const float*>(body)[j];
-        else if (h.fmt == FMT_Q8) x = lev_decode(reinterpret_cast<const uint8_t*>(body)[j], levels, h.norm, 0x80u);
-        else if (h.fmt == FMT_Q16) x = lev_decode(reinterpret_cast<const uint16_t*>(body)[j], levels, h.norm, 0x8000u);
+        if (fmt == FMT_F32) x = reinterpret_cast<const float*>(body)[j];
+        else if (fmt == FMT_Q8) x = lev_decode(reinterpret_cast<const uint8_t*>(body)[j], levels, s, norm, 0x80u);
+        else if (fmt == FMT_Q16) x = lev_decode(reinterpret_cast<const uint16_t*>(body)[j], levels, s, norm, 0x8000u);
         else x = nat_decode(reinterpret_cast<const uint16_t*>(body)[j]);
         out[j] = x;
     }
 }
 
-__global__ __launch_bounds__(256) void k_unpack_sparse(const char* __restrict__ payload, int64_t cap, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_unpack_sparse(const char* __restrict__ payload, int64_t cap, int64_t d,
+                                                       float* __restrict__ out) {
     const PayloadHeader h = *reinterpret_cast<const PayloadHeader*>(payload);
     const uint32_t* idx = reinterpret_cast<const uint32_t*>(payload + 16);
     const float* val = reinterpret_cast<const float*>(payload + 16 + a16(4 * cap));
     const int64_t cnt = min<int64_t>(h.count, cap);
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * blockDim.x)
-        out[idx[e]] = val[e];
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t j = idx[e];
+        if (j < (uint64_t)d) out[j] = val[e];                  // an index past the row is never written
+    }
 }
 
 // ---- decode + reduce over n payloads (dense formats) --------------------------------------------
@@ -190,15 +197,15 @@ struct WireFmt {
 };
 
 template <int FMT>
-__device__ inline float dec1(uint32_t c, const float* lv, float norm) {
-    if (FMT == FMT_Q8) return lev_decode(c, lv, norm, 0x80u);
-    if (FMT == FMT_Q16) return lev_decode(c, lv, norm, 0x8000u);
+__device__ inline float dec1(uint32_t c, const float* lv, int s, float norm) {
+    if (FMT == FMT_Q8) return lev_decode(c, lv, s, norm, 0x80u);
+    if (FMT == FMT_Q16) return lev_decode(c, lv, s, norm, 0x8000u);
     if (FMT == FMT_NAT16) return nat_decode(c);
     return __uint_as_float(c);
 }
 
 template <int FMT>
-__device__ inline void dec16(uint4 v, const float* lv, float norm, float* e) {
+__device__ inline void dec16(uint4 v, const float* lv, int s, float norm, float* e) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     constexpr int E = WireFmt<FMT>::E;
 #pragma unroll
@@ -207,7 +214,7 @@ __device__ inline void dec16(uint4 v, const float* lv, float norm, float* e) {
         if (FMT == FMT_Q8) c = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
         else if (FMT == FMT_F32) c = w[q];
         else c = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        e[q] = dec1<FMT>(c, lv, norm);
+        e[q] = dec1<FMT>(c, lv, s, norm);
     }
 }
 
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(256) void k_unpack_accum(const char* __restrict__ b
                     const float norm = (FMT == FMT_Q8 || FMT == FMT_Q16) ? sload(reinterpret_cast<const float*>(r + 8)) : 0.f;
                     const float wi = W ? w[i] : 1.f;
                     float e[E];
-                    dec16<FMT>(ring[p], lv, norm, e);
+                    dec16<FMT>(ring[p], lv, s, norm, e);
                     if (i + PF < n) ring[p] = *reinterpret_cast<const uint4*>(row(i + PF) + 16 + g * 16);
 #pragma unroll
                     for (int q = 0; q < E; ++q) {
@@ -276,7 +283,7 @@ __global__ __launch_bounds__(256) void k_unpack_accum(const char* __restrict__ b
                 if (FMT == FMT_Q8) c = reinterpret_cast<const uint8_t*>(r + 16)[j];
                 else if (FMT == FMT_F32) c = reinterpret_cast<const uint32_t*>(r + 16)[j];
                 else c = reinterpret_cast<const uint16_t*>(r + 16)[j];
-                const float e = dec1<FMT>(c, lv, norm);
+                const float e = dec1<FMT>(c, lv, s, norm);
                 const float t = W ? wi * e : e;
                 acc[q] = (i == 0) ? t : acc[q] + t;
             }
@@ -389,14 +396,65 @@ int unpack_run(const flc_codec_params* prm, const char* payload, int64_t d, floa
         const int64_t cap = std::max<int64_t>(1, std::min(prm->k, d));
         FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cap + 255) / 256, 4096));
-        hipLaunchKernelGGL(k_unpack_sparse, dim3(grid), dim3(256), 0, st, payload, cap, out);
+        hipLaunchKernelGGL(k_unpack_sparse, dim3(grid), dim3(256), 0, st, payload, cap, d, out);
         FLC_CHECK_LAUNCH("k_unpack_sparse");
         return FLC_OK;
     }
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 8192));
-    hipLaunchKernelGGL(k_unpack_dense, dim3(grid), dim3(256), 0, st, payload, d, prm->d_levels, out);
+    hipLaunchKernelGGL(k_unpack_dense, dim3(grid), dim3(256), 0, st, payload, d, fmt, prm->s, prm->d_levels, out);
     FLC_CHECK_LAUNCH("k_unpack_dense");
     return FLC_OK;
+}
+
+// Host check of one message as it comes off the network (flc_payload_validate): everything the
+// decode kernels take from the message itself — header format, count, the level codes, the sparse
+// indices — against what the codec and d allow.
+int payload_validate(const flc_codec_params* prm, const uint8_t* p, int64_t nbytes, int64_t d) {
+    const int64_t pb = payload_bytes(prm, d);
+    if (nbytes < pb) { set_error("payload: %lld bytes, the message of d=%lld is %lld", (long long)nbytes, (long long)d, (long long)pb); return FLC_ERR_ARG; }
+    if (d == 0) return FLC_OK;
+    PayloadHeader h;
+    std::memcpy(&h, p, sizeof h);
+    const int fmt = payload_format(prm);
+    if ((int)h.fmt != fmt) { set_error("payload: header format %u, the codec's is %d", h.fmt, fmt); return FLC_ERR_ARG; }
+    if (h.bad != 0u) { set_error("payload: %u elements flagged unrepresentable by the sender", h.bad); return FLC_ERR_ARG; }
+    const uint8_t* body = p + 16;
+    switch (fmt) {
+        case FMT_Q8:
+        case FMT_Q16: {
+            if (h.count != (uint32_t)d) { set_error("payload: count %u != d", h.count); return FLC_ERR_ARG; }
+            const uint32_t mask = fmt == FMT_Q8 ? 0x7Fu : 0x7FFFu;
+            for (int64_t j = 0; j < d; ++j) {
+                uint32_t c;
+                if (fmt == FMT_Q8) c = body[j];
+                else { uint16_t v; std::memcpy(&v, body + 2 * j, 2); c = v; }
+                if ((c & mask) > (uint32_t)prm->s) { set_error("payload: level code %u at %lld exceeds s=%d", c & mask, (long long)j, prm->s); return FLC_ERR_ARG; }
+            }
+            return FLC_OK;
+        }
+        case FMT_F32:
+        case FMT_NAT16:
+            if (h.count != (uint32_t)d) { set_error("payload: count %u != d", h.count); return FLC_ERR_ARG; }
+            return FLC_OK;
+        case FMT_SPARSE: {
+            const int64_t cap = std::max<int64_t>(1, std::min(prm->k, d));
+            if ((int64_t)h.count > cap) { set_error("payload: %u entries, at most K=%lld", h.count, (long long)cap); return FLC_ERR_ARG; }
+            int64_t prev = -1;
+            for (uint32_t e = 0; e < h.count; ++e) {
+                uint32_t j;
+                std::memcpy(&j, body + 4 * (int64_t)e, 4);
+                if ((int64_t)j >= d || (int64_t)j <= prev) { set_error("payload: entry %u index %u not ascending in [0, d)", e, j); return FLC_ERR_ARG; }
+                prev = j;
+            }
+            return FLC_OK;
+        }
+        case FMT_RANKK:
+            if ((int64_t)h.count != rk_rank(prm, d)) { set_error("payload: rank %u, the codec's is %lld", h.count, (long long)rk_rank(prm, d)); return FLC_ERR_ARG; }
+            return FLC_OK;
+        default:
+            set_error("payload: unknown format %d", fmt);
+            return FLC_ERR_UNSUPPORTED;
+    }
 }
 
 size_t unpack_reduce_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {

@@ -44,9 +44,10 @@ __device__ inline uint32_t lev_code(float v, const float* lv, int s, float norm,
     return neg ? sbit : 0u;
 }
 
-__device__ inline float lev_decode(uint32_t code, const float* lv, float norm, uint32_t sbit) {
+// a level index past s (only a malformed message has one) reads the top level, never past the table
+__device__ inline float lev_decode(uint32_t code, const float* lv, int s, float norm, uint32_t sbit) {
     if (code == 0u) return 0.f;
-    return lev_value(lv, code & (sbit - 1u), (code & sbit) != 0u, norm);
+    return lev_value(lv, min(code & (sbit - 1u), (uint32_t)s), (code & sbit) != 0u, norm);
 }
 
 // ---- natural codes ----------------------------------------------------------------------------

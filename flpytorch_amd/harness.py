@@ -44,12 +44,14 @@ client step is the fused shift codec (``Compressor.compressShift``, one flc_enco
 The others' serverGradient bodies are covered by ``aggregation.install``.
 """
 import math
+import threading
 
 import numpy as np
 import torch
 import torch.nn.functional as F
 
 from . import aggregation as ag
+from . import transport
 
 
 # ---------------------------------------------------------------------------------------------
@@ -221,8 +223,13 @@ class Simulation:
         # message (Compressor.compressPayload, include/flcodec.h layouts) and the server side
         # rebuilds it (decompressPayload, bit-exact) before the local step it applies — the
         # physical form of last_need_to_send_advance (the reference pickles dense tensors,
-        # comm_socket.py:16-82); bytes per client in client_state["stats"]["payload_bytes"]
-        self.wire = bool(wire)
+        # comm_socket.py:16-82); bytes per client in client_state["stats"]["payload_bytes"].
+        # wire="socket": the message also crosses a real socket (transport.PayloadSocket,
+        # CommSocket framing) and is checked against the codec on arrival (validatePayload)
+        if wire not in (False, True, "socket"):
+            raise ValueError(f"wire must be False, True or 'socket' (got {wire!r})")
+        self.wire = wire
+        self.link = transport.socket_pair() if wire == "socket" else None
         self.iterates = []                                                       # x after each round (opt-in)
         self.init_compressor = init_compressor or ag.initCompressor
         self.diana_step = diana_step or _on_gpu(ag.dianaStep)
@@ -285,6 +292,8 @@ class Simulation:
             if self.wire:
                 msg = comp.compressPayload(g)
                 cs["stats"]["payload_bytes"] = cs["stats"].get("payload_bytes", 0) + msg.numel()
+                if self.link is not None:
+                    msg = self.transfer(comp, msg, g.numel())
                 c = comp.decompressPayload(msg, g.numel())
             else:
                 c = comp.compressVector(g)
@@ -301,6 +310,28 @@ class Simulation:
         cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
         cs["g_prev"] = g_next
         return g_next
+
+    def transfer(self, comp, msg, d):
+        """One message client -> server over the socket pair: the client end sends on a thread
+        (a message larger than the socket buffer would otherwise block), the server end receives
+        and validates it; returns the received host uint8 tensor."""
+        client, server = self.link
+        err = []
+
+        def send():
+            try:
+                client.sendPayload(msg)
+            except Exception as e:                      # surfaced after the join
+                err.append(e)
+        t = threading.Thread(target=send)
+        t.start()
+        try:
+            got = server.recvPayload(comp, d)
+        finally:
+            t.join()
+        if err:
+            raise err[0]
+        return got
 
     # local_training (model_funcs.py:318-388) + train_model's loop (617-723)
     def local_training(self, cs, client_id):

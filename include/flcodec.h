@@ -206,6 +206,14 @@ int flc_pack(const flc_codec_params* prm, const flc_pattern* pat, const float* d
              void* d_payload, void* d_ws, size_t ws_bytes, void* stream);
 int flc_unpack(const flc_codec_params* prm, const void* d_payload, int64_t d, float* d_out,
                void* stream);
+/* Host-side check of a message received from a peer, before it goes to the device: nbytes >=
+ * flc_payload_bytes, header format = the codec's, bad = 0, count = d (dense formats) / <= K with
+ * strictly ascending indices < d (SPARSE) / the codec's rank (RANKK), level codes <= s (Q8 / Q16).
+ * FLC_OK or FLC_ERR_ARG with the reason in flc_last_error_string.  Host memory only; no device work.
+ * (The decode kernels also never index outside the row or the level table, whatever the bytes.)
+ * Replaces the trust the reference's transport places in pickle.loads of the peer's reply
+ * (model_funcs.py:445-452, comm_socket.py:59-82). */
+int flc_payload_validate(const flc_codec_params* prm, const void* h_payload, int64_t nbytes, int64_t d);
 size_t flc_unpack_reduce_workspace_size(const flc_codec_params* prm, int64_t n, int64_t d);
 int flc_unpack_reduce(const flc_codec_params* prm, const void* d_payloads, int64_t ld_bytes,
                       const void* const* d_payload_ptrs, int64_t n, int64_t d, const float* d_w,
