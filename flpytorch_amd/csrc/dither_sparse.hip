@@ -6,32 +6,45 @@
 // every row twice (norm pass + encode pass, codecs.hip).  But QSGD's output is sparse: element j
 // is nonzero only if y_j = |x_j| / ||x||_2 >= l1 (the first level, 1/s) or its draw goes up, so
 //     E[nonzeros] <= sum_j min(1, y_j / l1) <= ||x||_1 / (l1 ||x||_2) <= s sqrt(D)
-// for ANY row (2.5 % of the elements at s = 127, D = 25 M).  One streaming pass can therefore
-// accumulate the norm AND keep every element that could be nonzero, using a LOWER bound n_lo of
-// the norm (a spread sample's estimate, discounted): the candidates are then encoded exactly, with
-// the exact norm, by the chunk owners of the fold.
+// for ANY row (2.0 % of the elements at s = 127, D = 25 M for Gaussian rows).  One streaming pass
+// can therefore accumulate the norm AND decide almost every element, using BOUNDS n_lo <= n <=
+// n_hi of the norm from a spread sample (checked once the norm is known; a row outside its bounds
+// is folded dense):
 //
-//   sample  : per row, sum of squares of a spread 16 K-element sample -> n_lo, the candidate scale
-//             qc = 256 (1 + 2^-18) / (l1 n_lo), the device-RNG row key.
+//   sample  : per row, sum of squares (and 4th powers) of a spread 16 K-element sample -> n_lo,
+//             n_hi, the candidate scale qc = 256 (1 + 2^-18) / (l1 n_lo), the classification
+//             scales q0 = RU(1 / (l1 n_lo)), q1 = RD(1 / (l1 n_hi)), the device-RNG row key.
 //   filter  : ONE pass over every row: float64 sum of squares per 8192-element item (fixed slots),
-//             and every element passing  fma(|x|, qc, hi8) > 254.98  appended (idx, x) to the
-//             row's candidate list, per 4096-element chunk (tab[c][row]).  hi8 is the top byte of
-//             the element's draw (common.hpp: one group hash per 4 elements), so the test costs a
-//             quarter hash per element.
+//             and every element passing  fma(|x|, qc, hi8) > 254.98  staged in LDS (hi8 = the top
+//             byte of the element's draw, one group hash per 4 elements).  At the item's end each
+//             staged candidate is classified with its full 32-bit draw h (the low hash computed
+//             for the ~2 % staged only):
+//               sure   — kept at level l1 for EVERY norm in [n_lo, n_hi]: a 2-byte entry
+//                        (item-local index | sign) — its contribution is +-RN(l1 n) for any n;
+//               drop   — zero for every norm >= n_lo: nothing written;
+//               ambiguous (norm band, higher levels, 0-ish draws): the 8-byte (index | hi8, x).
 //   final   : per row, norm = RN(sqrt(sum of the partials in a fixed order)); the row is folded
-//             DENSE (every element re-read and encoded) if the norm is below n_lo (sample
-//             misjudged), not finite, its weight not finite, or its list overflowed.
-//   accum   : one wave owns a 4096-element chunk as an fp32 LDS tile and folds the rows in order:
-//             each candidate is encoded exactly (ds_encode = DitherOp::apply's arithmetic) and
-//             nonzero contributions are added; untouched columns get the sign of zero the
-//             sequential fold of the all-zero contributions gives (-0 only if every row gives -0).
+//             DENSE (every element re-read and encoded) if the norm is outside [n_lo, n_hi], not
+//             finite, its weight not finite, or an item overflowed its staging.
+//   resolve : the ambiguous entries encoded exactly with the norm (ds_encode = DitherOp::apply's
+//             arithmetic), rewritten in place as (index, C(x)) when nonzero.
+//   accum   : one wave owns a 2048-element half chunk as an fp32 LDS tile and folds the rows in
+//             order: per row its sure entries (+-RN(l1 n)) and resolved entries (C(x)), times the
+//             weight; untouched columns get the sign of zero the sequential fold of the all-zero
+//             contributions gives (-0 only if every row gives -0).
 //
-// The candidate test is conservative (never drops a nonzero).  For n >= n_lo, in the first level
-// interval [0, l1] the encode keeps l0 = 0 iff  h < ceil(p 2^32),  p = RN(RN(y - l1) / (-l1)),
-// y = RN(|x| / n), and  p >= 1 - y / l1 - 2^-23,  y <= (|x| / n_lo)(1 + 2^-24).  A nonzero output
-// has h >= p 2^32, so hi8 = h >> 24 > 256 p - 1 >= 255 - 256 |x| (1 + 2^-24) / (l1 n_lo) - 2^-15,
-// and  |x| qc + hi8 > 255 - 2^-15;  the fp32 fma loses < 2^-14 there, so  > 254.98  keeps every
-// nonzero.  Elements in higher intervals (y >= l1) have |x| qc >= 256.
+// Exactness of the classification.  In the first level interval [0, l1] the encode keeps l1 iff
+// h >= thr(n),  thr(n) = sat_u32(ceil(RN(RN(y - l1) / (-l1 2^-32)))),  y = RN(|x| / n).  Every
+// step is monotone, so thr is nondecreasing in n; and |thr(n) - 2^32 (1 - |x| / (n l1))| <
+// 2^32 2^-22.  Hence for n in [n_lo, n_hi] (and |x| q0 <= 1 - 2^-18, so y < l1 throughout):
+//   h / 2^32 + |x| / (n_hi l1) >= 1 + 2^-22  =>  kept for every such n      (sure)
+//   h / 2^32 + |x| / (n_lo l1) <  1 - 2^-22  =>  not kept for every such n  (drop)
+// evaluated as fp32 fmas with q1 / q0 and floor / ceil of h / 2^32 at 2^-24 resolution against
+// 1 +- 2^-20 (the fma's rounding is < 2^-24 there).  The candidate test itself is conservative (never
+// drops a nonzero): for n >= n_lo a nonzero output has h >= p 2^32 with p >= 1 - y / l1 - 2^-23,
+// so hi8 = h >> 24 > 255 - 256 |x| (1 + 2^-24) / (l1 n_lo) - 2^-15, and |x| qc + hi8 > 255 - 2^-15;
+// the fp32 fma loses < 2^-14 there, so > 254.98 keeps every nonzero.  Elements in higher
+// intervals (y >= l1) have |x| qc >= 256.
 #include <map>
 #include <mutex>
 #include <vector>
@@ -42,20 +55,32 @@
 namespace flc {
 
 constexpr uint32_t DS_DENSE = 1u, DS_FAST = 4u;
-constexpr int DS_FGS = 2;                  // chunks per filter work item (8192 elements; default)
+constexpr int DS_FGS = 2;                  // chunks per filter work item (8192 elements)
+constexpr int DS_NH = 2 * DS_FGS;          // fold tiles (half chunks) per item
 constexpr int DS_GCAP = 512;               // staged candidates per item (6.25 %; more -> row overflow)
+constexpr int DS_HCAP = DS_GCAP / DS_NH;    // entries per half chunk of an item (more -> row overflow)
+constexpr int DS_MAXLEV = 15;              // entry level field: 4 bits (a higher level -> row dense)
 constexpr int DS_SMAX = 16384;             // sample elements per row
 constexpr float DS_QT = 254.98f;
 constexpr int DS_MAXS = 512;               // level table entries kept in LDS by the fold
+constexpr uint32_t DS_OVF = 0xFFFFFFFFu;   // itm: the item overflowed its staging capacity
+constexpr int DS_AP = 8;                   // rows of entry lists in flight in the fold
 
+// One entry of the fold's lists (u16): half-chunk-local index (11 bits) | sign << 11 | level << 12;
+// its contribution is copysign(levels[level], sign) * norm — C(x) exactly as the encode forms it.
 struct DsWs {
-    uint2* tab;           // [H][N] (offset, count) of each row's candidates in half chunk h
-    uint2* ent;           // [N][cap] (entry word, x bits); word = chunk-local index (12 bits) |
-                          // the draw's top byte << 12
-    uint32_t* ovfi;       // [N][G] 1: the item overflowed its staging capacity
+    uint2* tabs;          // [Hp][N] (offset, count) of row's sure entries in half chunk h: the
+                          // list of (h, row) is ent16[row][offset .. offset + count + cntr)
+    uint32_t* cntr;       // [Hp][N] resolved entries appended after them (k_ds_resolve)
+    uint16_t* ent16;      // [N][cap] entries; item region = NH halves x DS_HCAP
+    uint2* enta;          // [N][cap] ambiguous candidates (item-local index | hi8 << 13, x bits)
+    uint32_t* itm;        // [G][N] ambiguous candidates of the item; DS_OVF: it overflowed
     uint32_t* flags;      // [N] DS_*
     float* qc;            // [N] candidate scale
-    float* nlo;           // [N] norm lower bound the scale assumes
+    float* nlo;           // [N] norm bounds the classification assumes (checked by k_ds_final)
+    float* nhi;
+    float* q0;            // [N] RU(1 / (l1 n_lo))
+    float* q1;            // [N] RD(1 / (l1 n_hi)); 0: no sure entries (n_hi unbounded)
     double* partial;      // [N][G] per-item sums of squares
     float* pn;            // [N] norm
     float* rpn;           // [N] RN(1 / norm)
@@ -63,10 +88,14 @@ struct DsWs {
     float* part;          // [D] running sums carried between the row groups' folds
     int64_t cap;          // per row: G * GCAP (each filter item owns a fixed region)
     int64_t G;            // filter items per row
+    int64_t n;            // rows
 };
 
 constexpr int HCHUNK = CHUNK / 2;          // the fold's tile: 2048 elements (8 KB of LDS per wave)
 __host__ __device__ inline int64_t nhalves(int64_t d) { return (d + HCHUNK - 1) / HCHUNK; }
+
+__device__ inline float f32_up(double v) { float f = (float)v; return (double)f < v ? nextafterf(f, __builtin_huge_valf()) : f; }
+__device__ inline float f32_down(double v) { float f = (float)v; return (double)f > v ? nextafterf(f, 0.f) : f; }
 
 // ------------------------------------------------------------------------------------------
 // Sample: one workgroup per row.
@@ -111,26 +140,38 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
         a2 = (r2[0] + r2[1]) + (r2[2] + r2[3]);
         a4 = (r4[0] + r4[1]) + (r4[2] + r4[3]);
         const float l0 = levels[0], l1 = levels[1];
-        const bool bad = !(l0 == 0.f) || !(l1 > 0.f);   // the bound needs levels 0 < l1 < ...
-        double nlo;
+        const bool bad = !(l0 == 0.f) || !(l1 > 0.f);   // the bounds need levels 0 < l1 < ...
+        double nlo, nhi = __builtin_huge_val();
         if (S == d) {
             nlo = sqrt(a2) * (1.0 - 0x1p-20);              // the whole row: the norm itself
+            nhi = sqrt(a2) * (1.0 + 0x1p-20);
         } else {
-            // estimate of the sum of squares, discounted by 6 sigma of the sample mean + 2 %
+            // estimate of the sum of squares, discounted by 6 sigma of the sample mean + 2 %; the
+            // upper bound only for light-tailed samples (heavy tails: n_hi unbounded, no sure entries)
             const double m = (double)S, mean2 = a2 / m;
             const double var = fmax(a4 / m - mean2 * mean2, 0.0);
             const double rel = sqrt(var / m) / mean2;      // NaN/inf when mean2 == 0 or overflow
             const double f = fmin(fmax(1.0 - 6.0 * rel - 0.02, 0.25), 0.97);
             nlo = sqrt(f * mean2 * (double)d);
+            if (rel <= 0.05) nhi = sqrt((1.0 + 6.0 * rel + 0.02) * mean2 * (double)d);
         }
         float nlof = (float)nlo;
         if (!(nlof >= 0.f) || !(nlof <= 3.0e38f)) nlof = 0.f;
+        float nhif = f32_up(nhi);
+        if (!(nhif >= nlof) || !(nhif <= 3.0e38f)) nhif = __builtin_huge_valf();
         const double qcd = 256.0 * (1.0 + 0x1p-18) / ((double)l1 * (double)nlof);   // +inf for nlof 0
         float qc = (float)(qcd * (1.0 + 0x1p-22));         // rounded up past the conversion
         if (!(qc >= 0.f)) qc = __builtin_huge_valf();
-        if (bad) qc = 0.f;                                 // row is folded dense anyway
+        float q0 = f32_up(1.0 / ((double)l1 * (double)nlof));                       // +inf for nlof 0
+        float q1 = f32_down(1.0 / ((double)l1 * (double)nhif));                     // 0 for nhi inf
+        if (!(q0 >= 0.f)) q0 = __builtin_huge_valf();
+        if (!(q1 >= 0.f) || !(q1 <= 3.0e38f)) q1 = 0.f;
+        if (bad) { qc = 0.f; q1 = 0.f; }                   // row is folded dense anyway
         ws.qc[row] = qc;
         ws.nlo[row] = nlof;
+        ws.nhi[row] = nhif;
+        ws.q0[row] = q0;
+        ws.q1[row] = q1;
         ws.flags[row] = bad ? DS_DENSE : 0u;
         ws.rk[row] = rowkey(client_key(seed, client0 + row));
     }
@@ -140,21 +181,21 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // Filter: a RING-deep buffer-load pipeline across chunks and items (select.hip's TopK filter
 // structure), the dithering candidate test and the norm.  A work item is DS_FGS consecutive
 // 4096-element chunks of one row; its candidates are compacted (ballot / mbcnt) into wave-private
-// LDS and copied out coalesced into the item's FIXED region of the row's list (item * GCAP): no
-// reservation atomic, so nothing returning sits in the in-order vmcnt queue of the load stream.
-// The tab gets one (offset, count) per 2048-element half chunk (the fold's tile).
+// LDS, classified (sure / drop / ambiguous) and copied out coalesced into the item's FIXED regions
+// of the row's lists (item * GCAP): no reservation atomic, so nothing returning sits in the
+// in-order vmcnt queue of the load stream.  The tab gets the sure entries' (offset, count) per
+// 2048-element half chunk (the fold's tile).
 // ------------------------------------------------------------------------------------------
-// PROBE (tuning runs only, FLC_DS_PROBE): 0 full; 1 no norm; 2 no candidate test (norm only);
-// 3 loads only (a running xor keeps them alive); 4 full but no copy-out of the staged entries;
-// 5 copy-out into one fixed per-wave scratch region (L2-resident: stores without HBM traffic);
-// 6 full with non-temporal copy-out stores
-template <int RING, int GCAP, int PROBE = 0, int FGS = DS_FGS>
-__global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, DsWs ws) {
-    constexpr int NH = 2 * FGS;                               // half chunks per item
+// PROBE (tuning build only, FLC_DS_PROBE; outputs NOT valid): 1 fp32 norm; 2 no candidate staging;
+// 3 loads + norm only
+template <int RING, int GCAP, int PROBE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, DsWs ws) {
+    constexpr int FGS = DS_FGS, NH = DS_NH;
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
-    static_assert(GCAP % 128 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
-    constexpr int DS_ITEM_STORES = 3 + GCAP / 128;          // partial, overflow, tab, copy-out
+    static_assert(GCAP % 512 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
+    constexpr int DS_ITEM_STORES = 4 + GCAP / 128;   // partial, itm, tab, sure and ambiguous copy-outs
     __shared__ uint2 stage[4][GCAP];                         // (entry word, x bits)
+    __shared__ __attribute__((aligned(16))) uint16_t stage16[4][GCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t G = ws.G;
@@ -164,6 +205,7 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
     if (it >= items) return;
     const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
     uint2* sg = stage[wv];
+    uint16_t* s16 = stage16[wv];
     float4 ring[RING];
     int64_t row = r0 + it / G;
     int64_t c = (it - (row - r0) * G) * FGS;
@@ -176,7 +218,7 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
     {
         // the stores an item ends with, dropped (num_records 0): the loop is entered with the same
         // vmcnt queue shape as it is re-entered
-        const auto nd = __builtin_amdgcn_make_buffer_rsrc(ws.ent, (short)0, 0, 0x00020000);
+        const auto nd = __builtin_amdgcn_make_buffer_rsrc(ws.enta, (short)0, 0, 0x00020000);
 #pragma unroll
         for (int k = 0; k < DS_ITEM_STORES; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, nd, lane * 4, k * 256, 0);
         __builtin_amdgcn_sched_barrier(0);
@@ -187,7 +229,6 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
         const int64_t gi = it - (row - r0) * G;
         const int64_t nit = it + stride;
         uint32_t cnt = 0;
-        uint32_t hc[NH];                                      // running count at each half's end
         double a2 = 0.0;
         int64_t nrow = row, nc = c;
 #pragma unroll
@@ -203,9 +244,9 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
             } else {
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
             }
-            // chunk-local index of (L, q): 4 lane + 256 L + q (opaque: keeps the 64 constants out
-            // of VGPRs); the entry word is that index | the draw's top byte << 12 (ds_encode)
-            uint32_t jb = (uint32_t)lane * 4u;
+            // item-local index of (L, q): 4096 sub + 4 lane + 256 L + q (opaque: keeps the 64
+            // constants out of VGPRs); the entry word is that index | the draw's top byte << 13
+            uint32_t jb = (uint32_t)lane * 4u + (uint32_t)sub * CHUNK;
             asm volatile("" : "+v"(jb));
             const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;   // hash input of L = 0
 #pragma unroll
@@ -217,20 +258,20 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if (PROBE == 0 || PROBE == 2) a2 = fma((double)vq[q], (double)vq[q], a2);
-                    if (PROBE == 3) { a2 = __longlong_as_double(__double_as_longlong(a2) ^ __float_as_uint(vq[q])); continue; }
-                    if (PROBE == 2) continue;
+                    if (PROBE == 1) a2 = (double)fmaf(vq[q], vq[q], (float)a2);
+                    else a2 = fma((double)vq[q], (double)vq[q], a2);
+                    if (PROBE == 3) continue;
                     const float hi = (float)((hg >> (8 * q)) & 0xFFu);
                     // no range test: past the row end the loads return 0, and a zero candidate
-                    // encodes to 0 (never folded); NaN from 0 * inf (qc = inf) is not a candidate
+                    // is dropped; NaN from 0 * inf (qc = inf) is not a candidate
                     const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
                     const uint64_t m = __ballot(f);
                     // position = cnt + candidates in lower lanes; an item past GCAP overflows (its
                     // row is folded dense), so wrapping is harmless
                     const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
-                    if (f) {
-                        const uint32_t word = ((((hg >> (8 * q)) & 0xFFu) << 12) | jb) + (uint32_t)(L * 256 + q);
+                    if (PROBE != 2 && f) {
+                        const uint32_t word = ((((hg >> (8 * q)) & 0xFFu) << 13) | jb) + (uint32_t)(L * 256 + q);
                         sg[pos] = make_uint2(word, __float_as_uint(vq[q]));
                     }
                     cnt += (uint32_t)__popcll(m);
@@ -238,46 +279,98 @@ __global__ __launch_bounds__(256) void k_ds_filter(RowSrc rows, int64_t n, int64
                 // keep the norm's fma chain here: left alone, the compiler sinks all 128 of an
                 // item's fmas to its end and holds the 128 x values live (218 VGPRs)
                 asm volatile("" : "+v"(a2));
-                if (L == 7) hc[2 * sub] = cnt;
-                if (L == 15) hc[2 * sub + 1] = cnt;
             }
             rs = rsn;
         }
         a2 = wave_sum(a2);                                   // fixed butterfly: deterministic
         const bool fits = cnt <= GCAP;
         const uint32_t base = (uint32_t)gi * GCAP;
+        // Classification of the staged candidates (LDS and ALU only: no vector-memory op between
+        // the item's loads and its fixed store sequence).  Sure entries go to stage16, half h's at
+        // h * DS_HCAP; ambiguous ones are compacted in place in sg (a batch reads its 64 slots
+        // before it writes lower ones).
+        uint32_t na = 0;
+        uint32_t hs[NH];
+#pragma unroll
+        for (int u = 0; u < NH; ++u) hs[u] = 0;
+        {
+            const float q0 = sload(ws.q0 + row), q1 = sload(ws.q1 + row);
+            const uint32_t rk2 = rk ^ 0x27D4EB2Fu;
+            const uint32_t j0 = (uint32_t)(gi * (FGS * CHUNK));
+            const uint32_t ncl = fits ? cnt : 0u;
+            for (uint32_t e0 = 0; e0 < ncl; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                const bool v = e < ncl;
+                const uint2 en = v ? sg[e] : make_uint2(0u, 0u);
+                const float x = __uint_as_float(en.y), ax = fabsf(x);
+                const uint32_t loc = en.x & 0x1FFFu;
+                const uint32_t h24 = ((en.x >> 13) << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);  // h >> 8
+                const float hf = (float)h24 * 0x1p-24f, hfu = (float)(h24 + 1u) * 0x1p-24f;
+                const bool inl = ax * q0 <= 1.0f - 0x1p-18f;
+                const bool nz = v && !(x == 0.f);
+                const bool sure = nz && inl && fmaf(ax, q1, hf) >= 1.0f + 0x1p-20f;
+                const bool drop = !nz || (inl && fmaf(ax, q0, hfu) < 1.0f - 0x1p-20f);
+                const bool amb = !sure && !drop;
+                const uint32_t u = loc >> 11;
+                uint32_t pin = 0;
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const uint64_t mh = __ballot(sure && u == (uint32_t)h);
+                    const uint32_t ph = __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, hs[h]));
+                    pin = u == (uint32_t)h ? ph : pin;
+                    hs[h] += (uint32_t)__popcll(mh);
+                }
+                if (sure && pin < (uint32_t)DS_HCAP)
+                    s16[u * DS_HCAP + pin] = (uint16_t)((loc & (HCHUNK - 1)) | ((en.y >> 31) << 11) | (1u << 12));
+                const uint64_t ma = __ballot(amb);
+                const uint32_t pa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, na));
+                if (amb) sg[pa] = en;
+                na += (uint32_t)__popcll(ma);
+            }
+        }
+        bool ovf = !fits;
+#pragma unroll
+        for (int u = 0; u < NH; ++u) ovf |= hs[u] > (uint32_t)DS_HCAP;
         // The item's stores: a FIXED sequence of DS_ITEM_STORES vector-memory ops with no exec
         // branch (every lane stores; duplicate lanes write equal values to equal addresses; the
-        // entry copy-out is range-checked by its buffer descriptor).  The stores sit in the
+        // copy-outs are range-checked by their buffer descriptors).  The stores sit in the
         // in-order vmcnt queue in front of the loads issued after them; with one fixed sequence on
         // every path (the prologue issues the same count of dropped stores) the compiler's static
         // vmcnt waits count them exactly instead of draining part of the ring.
         ws.partial[row * G + gi] = a2;
-        ws.ovfi[row * G + gi] = fits ? 0u : 1u;
+        ws.itm[gi * n + row] = ovf ? DS_OVF : na;
         {
-            const int u = lane & (NH - 1);
-            uint32_t lo = 0, hi = 0;
+            const uint32_t u = (uint32_t)lane & (NH - 1);
+            uint32_t hc = 0;
 #pragma unroll
-            for (int v = 0; v < NH; ++v) {
-                lo = v + 1 == u ? hc[v] : lo;
-                hi = v == u ? hc[v] : hi;
-            }
+            for (int v = 0; v < NH; ++v) hc = (uint32_t)v == u ? hs[v] : hc;
             // halves past the row end land in the tab's padding rows (G * NH >= H)
-            ws.tab[(gi * NH + u) * n + row] = make_uint2(base + lo, fits ? hi - lo : 0u);
+            ws.tabs[(gi * NH + u) * n + row] = make_uint2(base + u * DS_HCAP, ovf ? 0u : hc);
         }
         {
-            // two entries per lane per 16-B store; an odd count's last slot carries a stale entry
-            const uint32_t nrec = fits && PROBE != 4 ? ((cnt + 1u) & ~1u) * 8u : 0u;
-            uint2* dst = ws.ent + row * ws.cap + base;
-            if (PROBE == 5) dst = ws.ent + (((int64_t)blockIdx.x * 4 + wv) % 4096) * GCAP;
-            const auto od = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nrec, 0x00020000);
+            // sure entries: lane l holds entries 8 (l % 16) .. + 8 of half l / 16; slots past the
+            // half's count are sent out of range (dropped) by their offset, not by an exec branch
+            static_assert(DS_HCAP == 128 && GCAP == 512, "sure copy-out: 16 lanes x 16 B per half");
+            const uint32_t u = (uint32_t)lane >> 4, k8 = ((uint32_t)lane & 15u) * 8u;
+            uint32_t hc = 0;
+#pragma unroll
+            for (int v = 0; v < NH; ++v) hc = (uint32_t)v == u ? hs[v] : hc;
+            const bool put = !ovf && k8 < hc;
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.ent16 + row * ws.cap + base, (short)0, GCAP * 2, 0x00020000);
+            const uint4 v = reinterpret_cast<const uint4*>(s16)[lane];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od,
+                                                   put ? lane * 16 : 0x7FFFFFF0, 0, 0);
+        }
+        {
+            // ambiguous entries: two per lane per 16-B store; an odd count's last slot is stale
+            const uint32_t nrec = ovf ? 0u : ((na + 1u) & ~1u) * 8u;
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.enta + row * ws.cap + base, (short)0, (int)nrec, 0x00020000);
             const uint4* sq = reinterpret_cast<const uint4*>(sg);
 #pragma unroll
             for (int k = 0; k < GCAP / 128; ++k) {
                 const uint4 v = sq[k * 64 + lane];
                 __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od, (k * 64 + lane) * 16, 0,
-                    PROBE == 6 ? 2 : 0);
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od, (k * 64 + lane) * 16, 0, 0);
             }
         }
         // the copy-out reads precede the next item's staging writes in the wave's program order
@@ -298,7 +391,7 @@ __global__ __launch_bounds__(256) void k_ds_final(int64_t r0, int64_t rn, DsWs w
     if (row >= r0 + rn) return;
     double a = 0.0;
     uint32_t ov = 0;
-    for (int64_t k = lane; k < ws.G; k += 64) { a += ws.partial[row * ws.G + k]; ov |= ws.ovfi[row * ws.G + k]; }
+    for (int64_t k = lane; k < ws.G; k += 64) { a += ws.partial[row * ws.G + k]; ov |= ws.itm[k * ws.n + row] == DS_OVF; }
     a = wave_sum(a);
     ov = __ballot(ov != 0u) != 0ull;
     if (lane == 0) {
@@ -308,38 +401,10 @@ __global__ __launch_bounds__(256) void k_ds_final(int64_t r0, int64_t rn, DsWs w
         ws.rpn[row] = 1.0f / nv;
         uint32_t fl = ws.flags[row];
         const bool wbad = w && !(fabsf(w[row]) <= 3.4028235e38f);
-        if (!(nv >= ws.nlo[row]) || !(nv <= 3.4028235e38f) || ov || wbad) fl |= DS_DENSE;
+        if (!(nv >= ws.nlo[row]) || !(nv <= ws.nhi[row]) || !(nv <= 3.4028235e38f) || ov || wbad) fl |= DS_DENSE;
         if (nv >= 0x1p-40f && nv <= 0x1p80f) fl |= DS_FAST;   // |x| / norm may use div_fast
         ws.flags[row] = fl;
     }
-}
-
-// ------------------------------------------------------------------------------------------
-// Chunk-owner fold.  One wave per chunk, fp32 LDS tile, rows in order; per row the candidate list
-// (first 128 entries from a ring of AP rows in flight, the rest read in place) or, for DENSE rows,
-// the chunk of x itself.  Contributions are W ? w_i * C(x)_j : C(x)_j with C the exact encode.
-// ------------------------------------------------------------------------------------------
-constexpr int DS_AP = 8;                   // default rows of entry lists in flight (FLC_DS_AP: 8/16/32)
-
-struct DsMeta {
-    uint2 te;
-    float pn, rpn, w;
-    uint32_t rk, mode;
-};
-
-__device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t rend, int64_t r, const float* w) {
-    DsMeta m;
-    m.te = make_uint2(0, 0);
-    m.pn = 1.f; m.rpn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
-    if (r < rend) {
-        m.te = ws.tab[c * n + r];           // c: half-chunk index
-        m.pn = ws.pn[r];
-        m.rpn = ws.rpn[r];
-        m.rk = ws.rk[r];
-        m.mode = ws.flags[r];
-        if (w) m.w = w[r];
-    }
-    return m;
 }
 
 // Row state of the exact encode (wave-uniform).
@@ -349,14 +414,16 @@ struct DsRow {
     bool fast;            // norm inside the div_fast window
 };
 
-// C(x)_j of standard dithering (compressors.py:270-299) for one element, exactly as
-// DitherOp::apply<false> (codec_ops.hpp) computes it, specialised for the sparse fold: the draw's
-// top byte comes with the entry (hi8), and the rare slow cases (|x| or a level gap outside the
-// fast-division window, the interval guess off by one) are taken behind wave-level branches
-// instead of being if-converted.
-template <bool NOTAB = false>
-__device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow& r, const float4* tab, int s,
-                                  float sf) {
+// The level C(x)_j of standard dithering (compressors.py:270-299) picks for one element, exactly as
+// DitherOp::apply<false> (codec_ops.hpp) computes it: the draw's top byte comes with the entry
+// (hi8), and the rare slow cases (|x| or a level gap outside the fast-division window, the
+// interval guess off by one) are taken behind wave-level branches instead of being if-converted.
+// Returns the level's value (0 outside every interval) and index (-1 there).
+struct DsLev {
+    float v;
+    int idx;
+};
+__device__ inline DsLev ds_level(float x, uint32_t j, uint32_t hi8, const DsRow& r, const float4* tab, int s, float sf) {
     const float ax = fabsf(x);
     FastDiv dn;
     dn.b = r.n; dn.rb = r.rn; dn.ok = true;
@@ -367,7 +434,7 @@ __device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow
     }
     int g = (int)(y * sf);                                        // y >= 0; NaN -> 0
     g = g > s - 1 ? s - 1 : g;
-    float4 t = NOTAB ? make_float4((float)g, (float)g + 1.f, -0x1p-32f, -0x1p32f) : tab[g];
+    float4 t = tab[g];
     const bool off = (y < t.x) | (y > t.y);
     if (__builtin_expect(__ballot(off) != 0ull, 0)) {            // std levels RN(k/s): at most one off
         if (off) {
@@ -394,26 +461,164 @@ __device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow
     if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
         if (tie) down = ((hi8 << 24) | (fmix32(colbase(j) + r.rk2) >> 8)) < thr;
     }
-    const float lev = in ? (down ? t.x : t.y) : 0.f;
-    return (x == 0.f) ? 0.f : copysignf(lev, x) * r.n;           // (lev * sign(x)) * pnorm
+    DsLev l;
+    l.v = in ? (down ? t.x : t.y) : 0.f;
+    l.idx = in ? (down ? g : g + 1) : -1;
+    return l;
+}
+
+// C(x)_j: (lev * sign(x)) * pnorm
+__device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow& r, const float4* tab, int s, float sf) {
+    const DsLev l = ds_level(x, j, hi8, r, tab, s, sf);
+    return (x == 0.f) ? 0.f : copysignf(l.v, x) * r.n;
 }
 
 __device__ inline uint32_t ds_hi8(uint32_t j, uint32_t rk) { return (grouphash(j >> 2, rk) >> (8u * (j & 3u))) & 0xFFu; }
 
-// APROBE (tuning runs only, FLC_DS_APROBE; outputs invalid): 1 no encode (t = x); 2 no tile adds;
-// 3 encode without the level-table lookup; 4 no list fetch (constant in-range entries); 7 = 1+2+4
+// ------------------------------------------------------------------------------------------
+// Resolve: one wave per 64 filter items — item gi of 64 consecutive rows, one lane each, so the
+// per-item tables ([item][row]) are read and written coalesced; their ambiguous candidates,
+// spread over the wave's lanes, encoded with their rows' norms; the nonzero ones appended as list
+// entries after the sure entries of their half chunk (an LDS counter per (item, half): the order
+// inside one row's list is free, its columns are distinct), the counts into cntr.  A level above
+// DS_MAXLEV or a full half region turns the row dense.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_ds_resolve(int64_t n, int64_t r0, int64_t rn, DsWs ws,
+                                                    const float* __restrict__ levels, int s) {
+    constexpr int NH = DS_NH;
+    __shared__ __attribute__((aligned(16))) float4 tab[DS_MAXS];
+    __shared__ uint32_t pre[4][65], irow[4][64], igi[4][64], ikey[4][64], imode[4][64], cs[4][64][NH], cr[4][64][NH];
+    __shared__ float ipn[4][64], irpn[4][64];
+    load_table(levels, s, tab);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float sf = (float)s;
+    const int64_t nrb = (rn + 63) / 64, groups = nrb * ws.G;
+    for (int64_t grp = (int64_t)blockIdx.x * 4 + wv; grp < groups; grp += (int64_t)gridDim.x * 4) {
+        const uint32_t gi = (uint32_t)(grp / nrb);
+        const int64_t row = r0 + (grp - (int64_t)gi * nrb) * 64 + lane;
+        const bool valid = row < r0 + rn;
+        uint32_t na = 0, mode = DS_DENSE;
+        if (valid) {
+            mode = ws.flags[row];
+            if (!(mode & DS_DENSE)) na = ws.itm[(int64_t)gi * n + row];
+        }
+        // exclusive prefix of na over the lanes
+        uint32_t inc = na;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            inc += lane >= o ? t : 0u;
+        }
+        const uint32_t total = __shfl(inc, 63, 64);
+        pre[wv][lane] = inc - na;
+        if (lane == 0) pre[wv][64] = total;
+        irow[wv][lane] = (uint32_t)row;
+        igi[wv][lane] = gi;
+        ikey[wv][lane] = (valid ? ws.rk[row] : 0u) ^ 0x27D4EB2Fu;
+        imode[wv][lane] = mode;
+        ipn[wv][lane] = valid ? ws.pn[row] : 1.f;
+        irpn[wv][lane] = valid ? ws.rpn[row] : 1.f;
+#pragma unroll
+        for (int u = 0; u < NH; ++u) {
+            cs[wv][lane][u] = (na > 0u) ? ws.tabs[((int64_t)gi * NH + u) * n + row].y : 0u;
+            cr[wv][lane][u] = 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+            const uint32_t t = t0 + (uint32_t)lane;
+            const bool tv = t < total;
+            // the item of candidate t: the last k with pre[k] <= t
+            uint32_t k = 0;
+#pragma unroll
+            for (uint32_t step = 32; step > 0; step >>= 1)
+                if (pre[wv][k + step] <= t) k += step;
+            const uint32_t e = t - pre[wv][k];
+            const int64_t rk_ = irow[wv][k];
+            const uint32_t gk = igi[wv][k];
+            const int64_t ei = tv ? rk_ * ws.cap + (int64_t)gk * DS_GCAP + e : 0;         // lanes past the total: entry 0
+            uint2 en = ws.enta[ei];
+            if (!tv) en = make_uint2(0u, 0u);
+            const float x = __uint_as_float(en.y);
+            const uint32_t loc = en.x & 0x1FFFu;
+            DsRow rr;
+            rr.n = ipn[wv][k];
+            rr.rn = irpn[wv][k];
+            rr.rk2 = ikey[wv][k];
+            rr.fast = (imode[wv][k] & DS_FAST) != 0u;
+            const DsLev l = ds_level(x, gk * (uint32_t)(DS_FGS * CHUNK) + loc, en.x >> 13, rr, tab, s, sf);
+            const bool keep = tv && !(x == 0.f) && l.idx > 0 && !(l.v == 0.f);
+            if (keep) {
+                const uint32_t u = loc >> 11;
+                const uint32_t slot = atomicAdd(&cr[wv][k][u], 1u);
+                const uint32_t pos = cs[wv][k][u] + slot;
+                if (l.idx > DS_MAXLEV || pos >= (uint32_t)DS_HCAP) {
+                    atomicOr(&ws.flags[rk_], DS_DENSE);
+                } else {
+                    ws.ent16[rk_ * ws.cap + (int64_t)gk * DS_GCAP + u * DS_HCAP + pos] =
+                        (uint16_t)((loc & (HCHUNK - 1)) | ((en.y >> 31) << 11) | ((uint32_t)l.idx << 12));
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (valid && na > 0u) {
+#pragma unroll
+            for (int u = 0; u < NH; ++u) ws.cntr[((int64_t)gi * NH + u) * n + row] = cr[wv][lane][u];
+        } else if (valid) {
+#pragma unroll
+            for (int u = 0; u < NH; ++u) ws.cntr[((int64_t)gi * NH + u) * n + row] = 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Chunk-owner fold.  One wave per half chunk, fp32 LDS tile, rows in order; per row its list
+// (sure + resolved entries: copysign(levels[level], sign) * norm) — the first 64 entries from a
+// ring of AP rows in flight, the rest read in place — or, for DENSE rows, the half chunk of x
+// itself, encoded.  Contributions are W ? w_i * C(x)_j : C(x)_j.
+// ------------------------------------------------------------------------------------------
+struct DsMeta {
+    uint32_t off, cnt;
+    float pn, rpn, w;
+    uint32_t rk, mode;
+};
+
+__device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t rend, int64_t r, const float* w) {
+    DsMeta m;
+    m.off = 0; m.cnt = 0;
+    m.pn = 1.f; m.rpn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
+    if (r < rend) {
+        m.pn = ws.pn[r];
+        m.rpn = ws.rpn[r];
+        m.rk = ws.rk[r];
+        m.mode = ws.flags[r];
+        if (!(m.mode & DS_DENSE)) {                          // c: half-chunk index
+            const uint2 t = ws.tabs[c * n + r];
+            m.off = t.x;
+            m.cnt = t.y + ws.cntr[c * n + r];
+        }
+        if (w) m.w = w[r];
+    }
+    return m;
+}
+
 // Folds rows [r0, r0 + rn) into the running sums: the first group starts the tiles at -0, the others
 // continue from `part` (the previous group's tiles); the last group resolves untouched columns
 // over ALL n rows and writes out = sums / wt, the others write their tiles back to `part`.
-template <bool W, int AP, int APROBE = 0>
+template <bool W, int AP>
 __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
                                                   int64_t d, DsWs ws, const float* __restrict__ levels, int s,
                                                   const float* __restrict__ w, float wt, float* __restrict__ part,
                                                   float* __restrict__ out) {
     static_assert(64 % AP == 0, "row groups tile the 64-row batch");
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
     __shared__ __attribute__((aligned(16))) float tile[4][HCHUNK];
     __shared__ __attribute__((aligned(16))) float4 tab[DS_MAXS];
+    __shared__ float lvl[DS_MAXLEV + 1];
     load_table(levels, s, tab);
+    if (threadIdx.x <= (unsigned)DS_MAXLEV) lvl[threadIdx.x] = (int)threadIdx.x <= s ? levels[threadIdx.x] : 0.f;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t H = nhalves(d);
@@ -427,40 +632,31 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
         // -0 bit pattern marks exactly the untouched columns.  Zero contributions are not added.
         // Adds are read-modify-writes of the wave's own tile, in row order (one wave executes its
         // LDS operations in program order; the lanes of one instruction hit distinct columns), so
-        // each column sees its rows' terms in row order.  (ds_add_f32 atomics measured 30 % slower.)
+        // each column sees its rows' terms in row order.
         const uint32_t hbase = (uint32_t)(h * HCHUNK);
         const int64_t len = min((int64_t)HCHUNK, d - (int64_t)hbase);
         for (int i = lane; i < HCHUNK; i += 64) tl[i] = (first || i >= len) ? -0.f : part[hbase + i];
         DsMeta cur = ds_meta(ws, h, n, rend, r0 + lane, w), nxt;
-        uint32_t ri[AP];                        // ring: first 64 entries of the next AP rows' lists
-        float rv[AP];
+        uint32_t ra[AP];                        // ring: first 64 entries of the next AP rows' lists
+        // a list's 64-entry window never leaves its item's half region (DS_HCAP >= 64): loaded
+        // whole, lanes past the count dropped; an empty list (rows past the end, dense rows) reads
+        // the array's first 64 entries instead
         auto fetch = [&](const DsMeta& m, int q, int64_t row, int slot) {
-            if (APROBE == 4 || APROBE == 7) { ri[slot] = (uint32_t)lane * 29u & 2047u; rv[slot] = 0.01f * (float)lane; return; }
-            const uint32_t off = __builtin_amdgcn_readlane(m.te.x, q), cnt = __builtin_amdgcn_readlane(m.te.y, q);
-            const auto de = list_rsrc(ws.ent + row * ws.cap + off, 2 * cnt);
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(de, lane * 8, 0, 0);
-            ri[slot] = (uint32_t)lane < cnt ? v[0] : 0xFFFFFFFFu;       // invalid word: bits >= 20 set
-            rv[slot] = __uint_as_float(v[1]);
+            const uint32_t off = __builtin_amdgcn_readlane(m.off, q), cnt = __builtin_amdgcn_readlane(m.cnt, q);
+            const uint16_t* p = cnt ? ws.ent16 + row * ws.cap + off : ws.ent16;
+            const uint32_t v = p[lane];
+            ra[slot] = (uint32_t)lane < cnt ? v : NONE;
         };
         auto add = [&](uint32_t loc, float t) {
-            if (APROBE != 2 && APROBE != 7 && !(t == 0.f)) tl[loc] = tl[loc] + t;
+            if (!(t == 0.f)) tl[loc] = tl[loc] + t;
         };
-        auto row_state = [&](const DsMeta& m, int q, DsRow& rr, uint32_t& rk, uint32_t& mode, float& wi) {
-            rr.n = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.pn), q));
-            rr.rn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.rpn), q));
-            rk = __builtin_amdgcn_readlane(m.rk, q);
-            rr.rk2 = rk ^ 0x27D4EB2Fu;
-            mode = __builtin_amdgcn_readlane(m.mode, q);
-            rr.fast = (mode & DS_FAST) != 0u;
+        auto value = [&](uint32_t e, float pn) {            // copysign(levels[lev], sign) * pnorm
+            const float lv = lvl[e >> 12];
+            return __uint_as_float(__float_as_uint(lv) | ((e & 0x800u) << 20)) * pn;
+        };
+        auto row_state = [&](const DsMeta& m, int q, float& pn, float& wi) {
+            pn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.pn), q));
             wi = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.w), q));
-        };
-        auto contrib = [&](uint32_t word, float xv, const DsRow& rr, float wi) {
-            float t = 0.f;
-            if (word < (1u << 20)) {
-                const float e = (APROBE == 1 || APROBE == 7) ? xv : ds_encode<APROBE == 3>(xv, hbase + (word & (HCHUNK - 1)), word >> 12, rr, tab, s, sf);
-                t = W ? wi * e : e;
-            }
-            return t;
         };
 #pragma unroll
         for (int q = 0; q < AP; ++q) fetch(cur, q, r0 + q, q);
@@ -468,39 +664,41 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
             const int64_t i0 = r0 + b * 64;
             nxt = ds_meta(ws, h, n, rend, i0 + 64 + lane, w);
             // rows of this batch that need the general path: dense, or more than 64 entries here
-            const uint64_t slow = __ballot((i0 + lane < rend) && ((cur.mode & DS_DENSE) || cur.te.y > 64u));
+            const uint64_t slow = __ballot((i0 + lane < rend) && ((cur.mode & DS_DENSE) || cur.cnt > 64u));
             for (int qb = 0; qb < 64; qb += AP) {
                 const int nrow = (int)min((int64_t)AP, rend - (i0 + qb));
                 if (nrow == AP && ((slow >> qb) & ((AP == 64 ? 0ull : (1ull << AP)) - 1ull)) == 0ull) {
-                    // straight line: AP independent encodes (interleaved by the compiler), then
-                    // the adds in row order
+                    // straight line: AP rows' contributions, then the adds in row order
                     float t[AP];
 #pragma unroll
                     for (int u = 0; u < AP; ++u) {
-                        DsRow rr;
-                        uint32_t rk, mode;
-                        float wi;
-                        row_state(cur, qb + u, rr, rk, mode, wi);
-                        t[u] = contrib(ri[u], rv[u], rr, wi);
+                        float pn, wi;
+                        row_state(cur, qb + u, pn, wi);
+                        const float e = value(ra[u], pn);
+                        t[u] = W ? wi * e : e;
                     }
 #pragma unroll
                     for (int u = 0; u < AP; ++u)
-                        if (ri[u] < (1u << 20)) add(ri[u] & (HCHUNK - 1), t[u]);
+                        if (ra[u] != NONE) add(ra[u] & (HCHUNK - 1), t[u]);
                 } else {
                     for (int u = 0; u < nrow; ++u) {
                         const int q = qb + u;
                         const int64_t row = i0 + q;
-                        DsRow rr;
-                        uint32_t rk, mode;
-                        float wi;
-                        row_state(cur, q, rr, rk, mode, wi);
-                        uint32_t rw = 0xFFFFFFFFu;
-                        float rx = 0.f;
+                        float pn, wi;
+                        row_state(cur, q, pn, wi);
+                        const uint32_t mode = __builtin_amdgcn_readlane(cur.mode, q);
+                        uint32_t a = NONE;
 #pragma unroll
                         for (int z = 0; z < AP; ++z)
-                            if (z == u) { rw = ri[z]; rx = rv[z]; }
+                            if (z == u) a = ra[z];
                         if (mode & DS_DENSE) {
                             // dense row: every element of the half chunk, coalesced
+                            DsRow rr;
+                            rr.n = pn;
+                            rr.rn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.rpn), q));
+                            const uint32_t rk = __builtin_amdgcn_readlane(cur.rk, q);
+                            rr.rk2 = rk ^ 0x27D4EB2Fu;
+                            rr.fast = (mode & DS_FAST) != 0u;
                             const float* rp = rows.row(row) + hbase;
                             for (int k = 0; k < HCHUNK / 64; ++k) {
                                 const uint32_t e = (uint32_t)(k * 64 + lane);
@@ -510,12 +708,15 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
                                 }
                             }
                         } else {
-                            if (rw < (1u << 20)) add(rw & (HCHUNK - 1), contrib(rw, rx, rr, wi));
-                            const uint32_t cnt = __builtin_amdgcn_readlane(cur.te.y, q);
-                            const uint32_t off = __builtin_amdgcn_readlane(cur.te.x, q);
+                            if (a != NONE) {
+                                const float e = value(a, pn);
+                                add(a & (HCHUNK - 1), W ? wi * e : e);
+                            }
+                            const uint32_t cnt = __builtin_amdgcn_readlane(cur.cnt, q), off = __builtin_amdgcn_readlane(cur.off, q);
                             for (uint32_t e = 64u + lane; e < cnt; e += 64) {
-                                const uint2 en = ws.ent[row * ws.cap + off + e];
-                                add(en.x & (HCHUNK - 1), contrib(en.x, __uint_as_float(en.y), rr, wi));
+                                const uint32_t en = ws.ent16[row * ws.cap + off + e];
+                                const float ev = value(en, pn);
+                                add(en & (HCHUNK - 1), W ? wi * ev : ev);
                             }
                         }
                     }
@@ -558,42 +759,41 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
-// Filter variant.  The product build always takes the defaults; a -DFLC_TUNING build reads the
-// A/B switches once per process (FLC_DS_GCAP=1024 doubles the per-item staging and list regions,
-// FLC_DS_GRID=res launches a resident-only grid, FLC_DS_FGS=4 four-chunk items), so the
-// workspace query and the run always see the same variant.
-struct DsVariant { int gcap; bool resident; int ap; int fgs; int probe; int aprobe; int gridpct; };
+// Filter grid.  The product build always takes the default; a -DFLC_TUNING build reads the
+// A/B switches once per process (FLC_DS_GRID=res launches a resident-only grid; FLC_DS_GRIDPCT=p
+// caps it at p % of the resident blocks when row groups run).
+struct DsVariant { bool resident; int gridpct; int probe; };
 static const DsVariant& ds_variant() {
     static const DsVariant v = [] {
-        DsVariant r{DS_GCAP, false, DS_AP, DS_FGS, 0, 0, 100};
-        // FLC_DS_GRIDPCT=p: with row groups, the filter grid is capped at p % of the resident
-        // blocks so the previous group's fold finds free slots beside it
-        if (const char* e = tuning_env("FLC_DS_GRIDPCT")) r.gridpct = std::max(10, std::min(100, atoi(e)));
-        if (const char* e = tuning_env("FLC_DS_FGS")) r.fgs = atoi(e) == 4 ? 4 : DS_FGS;
-        if (const char* e = tuning_env("FLC_DS_AP")) r.ap = atoi(e);
-        if (const char* e = tuning_env("FLC_DS_GCAP")) r.gcap = atoi(e) == 1024 ? 1024 : DS_GCAP;
-        if (const char* e = tuning_env("FLC_DS_GRID")) r.resident = !strcmp(e, "res");
-        // probe modes measure parts of the filter / fold in isolation: their outputs are NOT valid
+        DsVariant r{false, 100, 0};
         if (const char* e = tuning_env("FLC_DS_PROBE")) r.probe = atoi(e);
-        if (const char* e = tuning_env("FLC_DS_APROBE")) r.aprobe = atoi(e);
+        if (const char* e = tuning_env("FLC_DS_GRIDPCT")) r.gridpct = std::max(10, std::min(100, atoi(e)));
+        if (const char* e = tuning_env("FLC_DS_GRID")) r.resident = !strcmp(e, "res");
         return r;
     }();
     return v;
 }
 
-static DsWs carve_ds(void* base, int64_t n, int64_t d, int gcap, int fgs, size_t* bytes) {
+static DsWs carve_ds(void* base, int64_t n, int64_t d, size_t* bytes) {
     Carver cv(base);
     const int64_t C = std::max<int64_t>(nchunks(d), 1), H = std::max<int64_t>(nhalves(d), 1);
     const int64_t nn = std::max<int64_t>(n, 1);
     DsWs w;
-    w.G = (C + fgs - 1) / fgs;
-    w.cap = w.G * gcap;
-    w.tab = cv.take<uint2>((size_t)std::max<int64_t>(H, w.G * 2 * fgs) * nn);   // + padding halves
-    w.ent = cv.take<uint2>((size_t)nn * w.cap);
-    w.ovfi = cv.take<uint32_t>((size_t)nn * w.G);
+    w.G = (C + DS_FGS - 1) / DS_FGS;
+    w.n = nn;
+    w.cap = w.G * DS_GCAP;
+    const size_t tabn = (size_t)std::max<int64_t>(H, w.G * DS_NH) * nn;         // + padding halves
+    w.tabs = cv.take<uint2>(tabn);
+    w.cntr = cv.take<uint32_t>(tabn);
+    w.ent16 = cv.take<uint16_t>((size_t)nn * w.cap);
+    w.enta = cv.take<uint2>((size_t)nn * w.cap);
+    w.itm = cv.take<uint32_t>((size_t)nn * w.G);
     w.flags = cv.take<uint32_t>(nn);
     w.qc = cv.take<float>(nn);
     w.nlo = cv.take<float>(nn);
+    w.nhi = cv.take<float>(nn);
+    w.q0 = cv.take<float>(nn);
+    w.q1 = cv.take<float>(nn);
     w.partial = cv.take<double>((size_t)nn * w.G);
     w.pn = cv.take<float>(nn);
     w.rpn = cv.take<float>(nn);
@@ -622,8 +822,7 @@ bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n,
 size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     (void)prm;
     size_t b = 0;
-    const DsVariant& v = ds_variant();
-    carve_ds(nullptr, n, d, v.gcap, v.fgs, &b);
+    carve_ds(nullptr, n, d, &b);
     return b;
 }
 
@@ -649,54 +848,42 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
            float wt, float* pnorm_out, float* out, void* wsp, size_t ws_bytes, hipStream_t st) {
     const DsVariant& v = ds_variant();
     size_t need = 0;
-    carve_ds(nullptr, n, d, v.gcap, v.fgs, &need);
+    carve_ds(nullptr, n, d, &need);
     if (ws_bytes < need) { set_error("dithering (sparse): workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
-    DsWs ws = carve_ds(wsp, n, d, v.gcap, v.fgs, nullptr);
+    DsWs ws = carve_ds(wsp, n, d, nullptr);
     const int64_t client0 = pat ? pat->client0 : 0;
     const int64_t H = nhalves(d);
-    const int probe = v.probe, aprobe = v.aprobe;
     const int K = ds_groups(prm, n);
 
     auto filter = [&](int64_t r0, int64_t rn) -> int {
-        auto launch = [&](auto kern) {
-            int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
-            if (v.resident || (K > 1 && v.gridpct < 100)) {
-                int per = 0, dev = 0, cus = 0;
-                if (hipGetDevice(&dev) == hipSuccess &&
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) == hipSuccess && per > 0)
-                    gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
-            }
-            ProfScope _ps("k_ds_filter", st);
-            hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, d, ws);
-        };
-        if (probe == 2) launch(k_ds_filter<16, DS_GCAP, 2>);
-        else if (probe == 3) launch(k_ds_filter<16, DS_GCAP, 3>);
-        else if (probe == 4) launch(k_ds_filter<16, DS_GCAP, 4>);
-        else if (probe == 5) launch(k_ds_filter<16, DS_GCAP, 5>);
-        else if (v.fgs == 4 && v.gcap == 1024) launch(k_ds_filter<16, 1024, 0, 4>);
-        else if (v.fgs == 4) launch(k_ds_filter<16, DS_GCAP, 0, 4>);
-        else if (v.gcap == 1024) launch(k_ds_filter<16, 1024>);
-        else launch(k_ds_filter<16, DS_GCAP>);
+        auto kern = v.probe == 1 ? k_ds_filter<16, DS_GCAP, 1> : v.probe == 2 ? k_ds_filter<16, DS_GCAP, 2>
+                  : v.probe == 3 ? k_ds_filter<16, DS_GCAP, 3> : k_ds_filter<16, DS_GCAP>;
+        int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
+        if (v.resident || (K > 1 && v.gridpct < 100)) {
+            int per = 0, dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) == hipSuccess && per > 0)
+                gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
+        }
+        { ProfScope _ps("k_ds_filter", st);
+        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, d, ws); }
         FLC_CHECK_LAUNCH("k_ds_filter");
         hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((rn + 3) / 4)), dim3(256), 0, st, r0, rn, ws, w, pnorm_out);
         FLC_CHECK_LAUNCH("k_ds_final");
+        const int rb = (int)std::max<int64_t>(1, std::min<int64_t>(((rn + 63) / 64 * ws.G + 3) / 4, 8192));
+        { ProfScope _ps("k_ds_resolve", st);
+        hipLaunchKernelGGL(k_ds_resolve, dim3(rb), dim3(256), 0, st, n, r0, rn, ws, prm->d_levels, prm->s); }
+        FLC_CHECK_LAUNCH("k_ds_resolve");
         return FLC_OK;
     };
     auto accum = [&](int64_t r0, int64_t rn, int first, int last, hipStream_t s2) -> int {
         const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + 3) / 4, 8192));
         ProfScope _ps("k_ds_accum", s2);
-        auto go = [&](auto kw, auto kn) {
-            if (w) hipLaunchKernelGGL(kw, dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels,
-                                      prm->s, w, wt, ws.part, out);
-            else hipLaunchKernelGGL(kn, dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels,
-                                    prm->s, w, wt, ws.part, out);
-        };
-        if (aprobe == 1) go(k_ds_accum<true, DS_AP, 1>, k_ds_accum<false, DS_AP, 1>);
-        else if (aprobe == 2) go(k_ds_accum<true, DS_AP, 2>, k_ds_accum<false, DS_AP, 2>);
-        else if (aprobe == 4) go(k_ds_accum<true, DS_AP, 4>, k_ds_accum<false, DS_AP, 4>);
-        else if (aprobe == 7) go(k_ds_accum<true, DS_AP, 7>, k_ds_accum<false, DS_AP, 7>);
-        else go(k_ds_accum<true, DS_AP>, k_ds_accum<false, DS_AP>);
+        if (w) hipLaunchKernelGGL((k_ds_accum<true, DS_AP>), dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d,
+                                  ws, prm->d_levels, prm->s, w, wt, ws.part, out);
+        else hipLaunchKernelGGL((k_ds_accum<false, DS_AP>), dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d,
+                                ws, prm->d_levels, prm->s, w, wt, ws.part, out);
         FLC_CHECK_LAUNCH("k_ds_accum");
         return FLC_OK;
     };
