@@ -94,6 +94,8 @@ struct DsWs {
 constexpr int HCHUNK = CHUNK / 2;          // the fold's tile: 2048 elements (8 KB of LDS per wave)
 __host__ __device__ inline int64_t nhalves(int64_t d) { return (d + HCHUNK - 1) / HCHUNK; }
 
+// top byte of element j's draw (common.hpp dev_draw)
+__device__ inline uint32_t ds_hi8(uint32_t j, uint32_t rk) { return (grouphash(j >> 2, rk) >> (8u * (j & 3u))) & 0xFFu; }
 __device__ inline float f32_up(double v) { float f = (float)v; return (double)f < v ? nextafterf(f, __builtin_huge_valf()) : f; }
 __device__ inline float f32_down(double v) { float f = (float)v; return (double)f > v ? nextafterf(f, 0.f) : f; }
 
@@ -207,8 +209,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     uint2* sg = stage[wv];
     uint16_t* s16 = stage16[wv];
     float4 ring[RING];
-    int64_t row = r0 + it / G;
-    int64_t c = (it - (row - r0) * G) * FGS;
+    // item it = (gi, row) with the row fastest: the waves in flight at any time read the same item
+    // of many rows, spread over the whole [N, D] block rather than one row's neighbouring items
+    int64_t row = r0 + it % rn;
+    int64_t c = (it / rn) * FGS;
     auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
 #pragma unroll
     for (int L = 0; L < RING - 1; ++L) {
@@ -226,7 +230,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     while (it < items) {
         const float qc = sload(ws.qc + row);
         const uint32_t rk = sload(ws.rk + row);
-        const int64_t gi = it - (row - r0) * G;
+        const int64_t gi = it / rn;
         const int64_t nit = it + stride;
         uint32_t cnt = 0;
         double a2 = 0.0;
@@ -238,14 +242,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             if (sub + 1 < FGS) {
                 rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
             } else if (nit < items) {
-                nrow = r0 + nit / G;
-                nc = (nit - (nrow - r0) * G) * FGS;
+                nrow = r0 + nit % rn;
+                nc = (nit / rn) * FGS;
                 rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
             } else {
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
             }
             // item-local index of (L, q): 4096 sub + 4 lane + 256 L + q (opaque: keeps the 64
-            // constants out of VGPRs); the entry word is that index | the draw's top byte << 13
+            // constants out of VGPRs); the draw's top byte is recomputed for the staged only
             uint32_t jb = (uint32_t)lane * 4u + (uint32_t)sub * CHUNK;
             asm volatile("" : "+v"(jb));
             const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;   // hash input of L = 0
@@ -271,8 +275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
                     if (PROBE != 2 && f) {
-                        const uint32_t word = ((((hg >> (8 * q)) & 0xFFu) << 13) | jb) + (uint32_t)(L * 256 + q);
-                        sg[pos] = make_uint2(word, __float_as_uint(vq[q]));
+                        sg[pos] = make_uint2(jb + (uint32_t)(L * 256 + q), __float_as_uint(vq[q]));
                     }
                     cnt += (uint32_t)__popcll(m);
                 }
@@ -304,7 +307,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                 const uint2 en = v ? sg[e] : make_uint2(0u, 0u);
                 const float x = __uint_as_float(en.y), ax = fabsf(x);
                 const uint32_t loc = en.x & 0x1FFFu;
-                const uint32_t h24 = ((en.x >> 13) << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);  // h >> 8
+                const uint32_t hi8 = ds_hi8(j0 + loc, rk);
+                const uint32_t h24 = (hi8 << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);   // h >> 8
                 const float hf = (float)h24 * 0x1p-24f, hfu = (float)(h24 + 1u) * 0x1p-24f;
                 const bool inl = ax * q0 <= 1.0f - 0x1p-18f;
                 const bool nz = v && !(x == 0.f);
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     s16[u * DS_HCAP + pin] = (uint16_t)((loc & (HCHUNK - 1)) | ((en.y >> 31) << 11) | (1u << 12));
                 const uint64_t ma = __ballot(amb);
                 const uint32_t pa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, na));
-                if (amb) sg[pa] = en;
+                if (amb) sg[pa] = make_uint2(loc | (hi8 << 13), en.y);      // k_ds_resolve's entry
                 na += (uint32_t)__popcll(ma);
             }
         }
@@ -473,7 +477,6 @@ __device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow
     return (x == 0.f) ? 0.f : copysignf(l.v, x) * r.n;
 }
 
-__device__ inline uint32_t ds_hi8(uint32_t j, uint32_t rk) { return (grouphash(j >> 2, rk) >> (8u * (j & 3u))) & 0xFFu; }
 
 // ------------------------------------------------------------------------------------------
 // Resolve: one wave per 64 filter items — item gi of 64 consecutive rows, one lane each, so the
