@@ -14,7 +14,8 @@ Workloads (BASELINE.json configs; the default is the largest single-GPU config, 
   c2  randk:1%  N=256  / GPU, D=1 M    (device-RNG indices)
   c4  qsgd:127  N=512  / GPU, D=25 M   (C4's per-GPU shard: at --gpus 8 this IS C4, N=4096)
   c5  randk:1% / topk:1% / qsgd:127 by client id mod 3, N=2048 / GPU, D=100 M (at --gpus 8: N=16384);
-      48 resident distinct rows replayed through the clients' row pointers; the per-group [D]
+      384 resident distinct rows (154 GB) replayed through the clients' row pointers (128 per codec
+      group: no kernel reads one row twice before ~GBs of other rows evict it); the per-group [D]
       partials are all-reduced asynchronously, overlapping the next group's encode
   reduce  ident N=512 / GPU, D=25 M   (the serverGradient fold alone)
 
@@ -53,7 +54,7 @@ WORKLOADS = {
                others=["k_ds_sample", "k_ds_accum"]),
     # C5: mixed per-client codec (client i -> specs[i % 3]); a pool of resident distinct rows is
     # replayed through the clients' row pointers (819 GB of distinct rows per GPU would not fit)
-    "c5": dict(spec="mixed", specs=["randk:1%", "topk:1%", "qsgd:127"], n=2048, d=100_000_000, pool=48,
+    "c5": dict(spec="mixed", specs=["randk:1%", "topk:1%", "qsgd:127"], n=2048, d=100_000_000, pool=384,
                kernel="k_ds_filter", config=4,
                others=["k_topk_filter", "k_randk_counts", "k_randk_fold", "k_ds_accum", "k_chunk_accum"]),
     # the serverGradient fold alone (identity codec), C4's shard shape

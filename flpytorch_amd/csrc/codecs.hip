@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, const float* 
         if (VEC) {
             const int64_t g0 = j0 / 4, g1 = j1 / 4;   // j0 % 4 == 0 (plen % 4 == 0)
             for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
-                float4 v = reinterpret_cast<const float4*>(r)[g];
+                float4 v = ld_row4(reinterpret_cast<const float4*>(r) + g);
                 if (DIFF) {
                     const float4 u = reinterpret_cast<const float4*>(sub)[g];
                     v = make_float4(v.x - u.x, v.y - u.y, v.z - u.z, v.w - u.w);
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_ew_accum_vec(RowSrc src, int64_t n, int
             if (p < n) {
                 const float4* r = reinterpret_cast<const float4*>(src.row(p));
 #pragma unroll
-                for (int c = 0; c < COLS; ++c) ring[p][c] = ok[c] ? r[gi[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int c = 0; c < COLS; ++c) ring[p][c] = ok[c] ? ld_row4(r + gi[c]) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
         float4 acc[COLS];
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void k_ew_accum_vec(RowSrc src, int64_t n, int
                     if (i + PF < n) {
                         const float4* r = reinterpret_cast<const float4*>(src.row(i + PF));
 #pragma unroll
-                        for (int c = 0; c < COLS; ++c) ring[p][c] = ok[c] ? r[gi[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        for (int c = 0; c < COLS; ++c) ring[p][c] = ok[c] ? ld_row4(r + gi[c]) : make_float4(0.f, 0.f, 0.f, 0.f);
                     }
                 }
             }

@@ -65,6 +65,10 @@ constexpr float DS_QT = 254.98f;
 constexpr int DS_MAXS = 512;               // level table entries kept in LDS by the fold
 constexpr uint32_t DS_OVF = 0xFFFFFFFFu;   // itm: the item overflowed its staging capacity
 constexpr int DS_AP = 8;                   // rows of entry lists in flight in the fold
+// rows per block of the filter's item order: 16 measured as fast as one block of all rows at C4
+// (and 1, row-major, 1-2 % slower on the same box); a block never reads one row twice, so rows
+// that alias (C5's replayed pool) are still read from HBM once per client
+constexpr int64_t DS_RB = 16;
 
 // One entry of the fold's lists (u16): half-chunk-local index (11 bits) | sign << 11 | level << 12;
 // its contribution is copysign(levels[level], sign) * norm — C(x) exactly as the encode forms it.
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // PROBE (tuning build only, FLC_DS_PROBE; outputs NOT valid): 1 fp32 norm; 2 no candidate staging;
 // 3 loads + norm only
 template <int RING, int GCAP, int PROBE = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, DsWs ws) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws) {
     constexpr int FGS = DS_FGS, NH = DS_NH;
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     static_assert(GCAP % 512 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
@@ -209,10 +213,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     uint2* sg = stage[wv];
     uint16_t* s16 = stage16[wv];
     float4 ring[RING];
-    // item it = (gi, row) with the row fastest: the waves in flight at any time read the same item
-    // of many rows, spread over the whole [N, D] block rather than one row's neighbouring items
-    int64_t row = r0 + it % rn;
-    int64_t c = (it / rn) * FGS;
+    // item order: blocks of rb rows (the last one shorter), and inside a block (gi, row) with the
+    // row fastest: the waves in flight at any time read the same item of the block's rows, spread
+    // over rb rows rather than one row's neighbouring items, and each row is read once per launch
+    // even when rows alias (a row read twice inside one block would be served from the caches)
+    auto item_at = [&](int64_t t, int64_t& r, int64_t& g) {
+        const int64_t blk = t / (rb * G), rem = t - blk * rb * G;
+        const int64_t bn = min(rb, rn - blk * rb);            // rows in this block
+        g = rem / bn;
+        r = r0 + blk * rb + (rem - g * bn);
+    };
+    int64_t row, gi0;
+    item_at(it, row, gi0);
+    int64_t c = gi0 * FGS;
     auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
 #pragma unroll
     for (int L = 0; L < RING - 1; ++L) {
@@ -230,7 +243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     while (it < items) {
         const float qc = sload(ws.qc + row);
         const uint32_t rk = sload(ws.rk + row);
-        const int64_t gi = it / rn;
+        const int64_t gi = c / FGS;
         const int64_t nit = it + stride;
         uint32_t cnt = 0;
         double a2 = 0.0;
@@ -242,8 +255,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             if (sub + 1 < FGS) {
                 rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
             } else if (nit < items) {
-                nrow = r0 + nit % rn;
-                nc = (nit / rn) * FGS;
+                int64_t ngi;
+                item_at(nit, nrow, ngi);
+                nc = ngi * FGS;
                 rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
             } else {
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
@@ -765,10 +779,11 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
 // Filter grid.  The product build always takes the default; a -DFLC_TUNING build reads the
 // A/B switches once per process (FLC_DS_GRID=res launches a resident-only grid; FLC_DS_GRIDPCT=p
 // caps it at p % of the resident blocks when row groups run).
-struct DsVariant { bool resident; int gridpct; int probe; };
+struct DsVariant { bool resident; int gridpct; int probe; int64_t rb; };
 static const DsVariant& ds_variant() {
     static const DsVariant v = [] {
-        DsVariant r{false, 100, 0};
+        DsVariant r{false, 100, 0, DS_RB};
+        if (const char* e = tuning_env("FLC_DS_RB")) r.rb = std::max<int64_t>(1, atoll(e));
         if (const char* e = tuning_env("FLC_DS_PROBE")) r.probe = atoi(e);
         if (const char* e = tuning_env("FLC_DS_GRIDPCT")) r.gridpct = std::max(10, std::min(100, atoi(e)));
         if (const char* e = tuning_env("FLC_DS_GRID")) r.resident = !strcmp(e, "res");
@@ -870,7 +885,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
                 gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
         }
         { ProfScope _ps("k_ds_filter", st);
-        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, d, ws); }
+        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, std::min<int64_t>(v.rb, rn), d, ws); }
         FLC_CHECK_LAUNCH("k_ds_filter");
         hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((rn + 3) / 4)), dim3(256), 0, st, r0, rn, ws, w, pnorm_out);
         FLC_CHECK_LAUNCH("k_ds_final");

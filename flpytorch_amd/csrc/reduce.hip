@@ -32,14 +32,14 @@ __global__ __launch_bounds__(256) void k_reduce_vec(RowSrc src, int64_t n, int64
         if (MODE == FLC_REDUCE_REL_X) xv = reinterpret_cast<const float4*>(x)[g];
         float4 acc;
         {
-            float4 r = reinterpret_cast<const float4*>(src.row(0))[g];
+            float4 r = ld_row4(reinterpret_cast<const float4*>(src.row(0)) + g);
             acc = term<MODE>(r, xv, w ? w[0] : 1.f);
         }
         int64_t i = 1;
         for (; i + UNROLL <= n; i += UNROLL) {
             float4 r[UNROLL];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) r[u] = reinterpret_cast<const float4*>(src.row(i + u))[g];
+            for (int u = 0; u < UNROLL; ++u) r[u] = ld_row4(reinterpret_cast<const float4*>(src.row(i + u)) + g);
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
                 float4 t = term<MODE>(r[u], xv, w ? w[i + u] : 1.f);
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void k_reduce_vec(RowSrc src, int64_t n, int64
             }
         }
         for (; i < n; ++i) {
-            float4 t = term<MODE>(reinterpret_cast<const float4*>(src.row(i))[g], xv, w ? w[i] : 1.f);
+            float4 t = term<MODE>(ld_row4(reinterpret_cast<const float4*>(src.row(i)) + g), xv, w ? w[i] : 1.f);
             acc.x = acc.x + t.x; acc.y = acc.y + t.y; acc.z = acc.z + t.z; acc.w = acc.w + t.w;
         }
         reinterpret_cast<float4*>(out)[g] = make_float4(acc.x / wt, acc.y / wt, acc.z / wt, acc.w / wt);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the current csrc tree as an A/B variant library flpytorch_amd/libflcodec_<tag>.so (loaded
-# with FLC_LIB_VARIANT=<tag>); the product libflcodec.so is untouched.   usage: tools/ab_build.sh <tag>
+# with FLC_LIB_VARIANT=<tag>); the product libflcodec.so is untouched.   usage: [XFLAGS=-D...] tools/ab_build.sh <tag>
 set -e
 tag=$1
 root=$(cd "$(dirname "$0")/.." && pwd)
@@ -8,5 +8,5 @@ tmp=/tmp/ab_$tag
 rm -rf $tmp && mkdir -p $tmp/flpytorch_amd $tmp/include
 cp -r $root/flpytorch_amd/csrc $tmp/flpytorch_amd/ && rm -rf $tmp/flpytorch_amd/csrc/build $tmp/flpytorch_amd/csrc/build_tuning
 cp $root/include/flcodec.h $tmp/include/
-make -s -j8 -C $tmp/flpytorch_amd/csrc BUILD=$tmp/build OUT=$root/flpytorch_amd/libflcodec_$tag.so
+make -s -j8 -C $tmp/flpytorch_amd/csrc BUILD=$tmp/build OUT=$root/flpytorch_amd/libflcodec_$tag.so XFLAGS="$XFLAGS"
 echo "built flpytorch_amd/libflcodec_$tag.so"
