@@ -199,6 +199,19 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
 // path.  Result as k_radix_select's last pass: thr = K-th key, krem = ties to admit, F_TIES when
 // the list has more keys equal to thr than that.
 // ------------------------------------------------------------------------------------------
+// candidate values of a row, read twice per launch (measured: nt loads 0.335 -> 0.293 ms at C3)
+#ifndef FLC_CS_NT
+#define FLC_CS_NT 1
+#endif
+__device__ inline float4 cs_ld(const float4* p) {
+#if FLC_CS_NT
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
 template <int NT>
 __global__ __launch_bounds__(NT) void k_cand_select(int64_t n, int64_t K, SelWs ws) {
     __shared__ uint32_t h[HBINS];
@@ -235,7 +248,7 @@ __global__ __launch_bounds__(NT) void k_cand_select(int64_t n, int64_t K, SelWs 
             for (; i + 7 * NT < n4; i += 8 * NT) {
                 float4 q[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) q[u] = v4[i + u * NT];
+                for (int u = 0; u < 8; ++u) q[u] = cs_ld(v4 + i + u * NT);
 #pragma unroll
                 for (int u = 0; u < 8; ++u) { add(q[u].x); add(q[u].y); add(q[u].z); add(q[u].w); }
             }
@@ -444,7 +457,7 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 // num_records 0 and its loads return zeros without touching memory).
 // FGS: chunks per work item (group).
 template <int RING, int FGS>
-__global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
+__global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     __shared__ uint32_t st_idx[2][4][GCAP];
     __shared__ float st_val[2][4][GCAP];
@@ -457,8 +470,17 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
     int64_t it = (int64_t)blockIdx.x * 4 + wv;
     if (it >= items) return;
     float4 ring[RING];
-    int64_t row = it / G;
-    int64_t c = (it - row * G) * FGS;                                    // current chunk
+    // item order: blocks of rb rows, inside a block (group, row) with the row fastest (rb = 1:
+    // row-major)
+    auto item_at = [&](int64_t t, int64_t& r, int64_t& cc) {
+        const int64_t blk = t / (rb * G), rem = t - blk * rb * G;
+        const int64_t bn = min(rb, n - blk * rb);
+        const int64_t g = rem / bn;
+        r = blk * rb + (rem - g * bn);
+        cc = g * FGS;
+    };
+    int64_t row, c;                                                      // current row, chunk
+    item_at(it, row, c);
     auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
 #pragma unroll
     for (int L = 0; L < RING - 1; ++L) {
@@ -524,8 +546,7 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
             if (sub + 1 < FGS) {
                 rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
             } else if (nit < items) {
-                nrow = nit / G;
-                nc = (nit - nrow * G) * FGS;
+                item_at(nit, nrow, nc);
                 rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
             } else {
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
@@ -1043,7 +1064,7 @@ __device__ void resolve_neg_zero(float* tl, uint32_t* rm, const SelWs& ws, int64
 
 // TS < CHUNK: a wave owns TS columns of a chunk (CHUNK / TS waves read the same lists and each
 // folds its part): a smaller LDS tile per wave, so more waves per CU hide the list latency.
-template <bool ASSIGN, int TS = CHUNK>
+template <bool ASSIGN, int TS = CHUNK, bool W = true>
 __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
                                                      float wt, float* __restrict__ out) {
     constexpr int PARTS = CHUNK / TS;
@@ -1081,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
             const uint32_t key = mag_key(vv);
             if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut))) {
                 if (ASSIGN) tl[loc] = vv;
-                else tl[loc] = tl[loc] + wi * vv;
+                else tl[loc] = W ? tl[loc] + wi * vv : tl[loc] + vv;
             }
         };
 #pragma unroll
@@ -1097,7 +1118,7 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
                     const uint32_t T = __builtin_amdgcn_readlane(cur.thr, q);
                     const uint32_t cut = __builtin_amdgcn_readlane(cur.cut, q);
                     const uint32_t mode = __builtin_amdgcn_readlane(cur.mode, q);
-                    const float wi = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.w), q));
+                    const float wi = W ? __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.w), q)) : 1.f;
                     fold(ri[slot][0], rv[slot][0], T, cut, mode, wi);
                     fold(ri[slot][1], rv[slot][1], T, cut, mode, wi);
                     if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, slot);
@@ -1110,7 +1131,7 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
                     const uint32_t T = __shfl(cur.thr, q, WAVE), cut = __shfl(cur.cut, q, WAVE);
                     const uint32_t mode = __shfl(cur.mode, q, WAVE), cnt = __shfl(cur.te.y, q, WAVE);
                     const uint32_t off = __shfl(cur.te.x, q, WAVE);
-                    const float wi = __shfl(cur.w, q, WAVE);
+                    const float wi = W ? __shfl(cur.w, q, WAVE) : 1.f;
                     uint32_t i_0 = 0, i_1 = 0;
                     float v_0 = 0.f, v_1 = 0.f;
 #pragma unroll
@@ -1576,7 +1597,12 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream
     // the hardware dispatcher balances the tail)
     const int64_t waves = n * ((nchunks(d) + FGS - 1) / FGS);
     const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 32768));
-    hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, d, ws);
+    static const int64_t rb = [] {
+        // rows per block of the item order: 64 measured 0.5 % faster than row-major (1) at C3
+        const char* e = tuning_env("FLC_TK_RB");          // tuning runs only
+        return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
+    }();
+    hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, std::min(rb, std::max<int64_t>(n, 1)), d, ws);
 }
 
 static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
@@ -1668,19 +1694,16 @@ static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const
     // the latency-bound row walk runs on more of the chip (many chunks: one wave each, measured best)
     int parts = accum_parts();
     if (parts == 0) parts = C >= 1024 ? 1 : (C >= 256 ? 2 : 4);
-    if (parts == 4) {
-        const int ab = grid_stride_blocks((4 * C + 3) / 4, 8192);
-        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 4>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    } else if (parts == 2) {
-        const int ab = grid_stride_blocks((2 * C + 3) / 4, 8192);
-        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK / 2>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    } else {
-        const int ab = grid_stride_blocks((C + 3) / 4, 4096);
-        if (assign) hipLaunchKernelGGL((k_chunk_accum<true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
-    } }
+    auto go = [&](auto ts, int ab) {
+        constexpr int TS = decltype(ts)::value;
+        if (assign) hipLaunchKernelGGL((k_chunk_accum<true, TS>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else if (w) hipLaunchKernelGGL((k_chunk_accum<false, TS, true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false, TS, false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out);
+    };
+    if (parts == 4) go(std::integral_constant<int, CHUNK / 4>{}, grid_stride_blocks((4 * C + 3) / 4, 8192));
+    else if (parts == 2) go(std::integral_constant<int, CHUNK / 2>{}, grid_stride_blocks((2 * C + 3) / 4, 8192));
+    else go(std::integral_constant<int, CHUNK>{}, grid_stride_blocks((C + 3) / 4, 4096));
+    }
     FLC_CHECK_LAUNCH("k_chunk_accum");
     return FLC_OK;
 }
