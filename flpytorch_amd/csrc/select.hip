@@ -685,6 +685,136 @@ __global__ void k_build_worklist(int64_t n, int64_t K, int64_t d, SelWs ws, int 
     if (threadIdx.x == 0) *ws.nwork = cnt;
 }
 
+// Exact path of the fast path's rare failures, in ONE launch: a workgroup per row (grid-stride),
+// rows without F_OVERFLOW / F_SHORT return at once.  A failed row gets the exact radix select over
+// its full row (three 11/11/9-bit passes, LDS histogram), then its list is rewritten chunk by
+// chunk in index order: key > thr, plus the first krem elements with key == thr (the lowest
+// indices, the oracle's tie rule), tab[c][row] = (offset, count), flags = F_EXACT (the fold admits
+// the whole list).  The same selection as the multi-launch path (k_build_worklist, k_radix_*,
+// k_tie_*, k_topk_filter<true>) that dense-K rows take, without its ~10 launches per call when no
+// row failed.
+constexpr int EX_NT = 1024;
+constexpr int EX_U = 8;                      // float4 loads per thread in flight in the radix passes
+
+// exclusive prefix of v over the workgroup's threads (in thread order) and the total
+__device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [EX_NT / 64] */, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        inc += lane >= o ? t : 0u;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < EX_NT / 64; ++k) {
+        const uint32_t x = wsum[k];
+        before += k < wv ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    total = tot;
+    return before + inc - v;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t wsum[EX_NT / 64];
+    const int t = threadIdx.x;
+    const int64_t C = nchunks(d);
+    for (int64_t row = blockIdx.x; row < n; row += gridDim.x) {
+        if (!(ws.flags[row] & (F_OVERFLOW | F_SHORT))) continue;       // row-uniform
+        const float* r = rows.row(row);
+        uint32_t prefix = 0, krem = (uint32_t)K;
+        for (int p = 0; p < 3; ++p) {
+            for (int i = t; i < HBINS; i += EX_NT) h[i] = 0;
+            __syncthreads();
+            auto add = [&](uint32_t k) { if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u); };
+            int64_t j = 0;
+            if (VEC) {
+                const float4* r4 = reinterpret_cast<const float4*>(r);
+                const int64_t g4 = d / 4;
+                int64_t g = t;
+                for (; g + (EX_U - 1) * EX_NT < g4; g += EX_U * EX_NT) {
+                    float4 q[EX_U];
+#pragma unroll
+                    for (int u = 0; u < EX_U; ++u) q[u] = ld_row4(r4 + g + u * EX_NT);
+#pragma unroll
+                    for (int u = 0; u < EX_U; ++u) {
+                        add(mag_key(q[u].x)); add(mag_key(q[u].y)); add(mag_key(q[u].z)); add(mag_key(q[u].w));
+                    }
+                }
+                for (; g < g4; g += EX_NT) {
+                    const float4 q = ld_row4(r4 + g);
+                    add(mag_key(q.x)); add(mag_key(q.y)); add(mag_key(q.z)); add(mag_key(q.w));
+                }
+                j = g4 * 4;
+            }
+            for (int64_t jj = j + t; jj < d; jj += EX_NT) add(mag_key(r[jj]));
+            __syncthreads();
+            uint32_t bin, above;
+            hist_find(h, krem, bin, above, scratch);
+            prefix = (prefix << pass_bits(p)) | bin;                   // p == 0: prefix is 0
+            krem -= above;
+            __syncthreads();
+        }
+        const uint32_t thr = prefix;                                    // the K-th key; krem ties admitted
+        uint32_t* oi = ws.ent_idx + row * ws.cap;
+        float* ov = ws.ent_val + row * ws.cap;
+        uint32_t base = 0, tie_run = 0;
+        for (int64_t c = 0; c < C; ++c) {
+            const int64_t j0 = c * CHUNK + (int64_t)t * 4;
+            float v[4];
+            if (VEC && j0 + 3 < d) {
+                const float4 q = ld_row4(reinterpret_cast<const float4*>(r + j0));
+                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = (j0 + q < d) ? r[j0 + q] : 0.f;
+            }
+            bool gt[4], eq[4];
+            uint32_t ne = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool in = j0 + q < d;
+                const uint32_t k = mag_key(v[q]);
+                gt[q] = in && k > thr;
+                eq[q] = in && k == thr;
+                ne += eq[q] ? 1u : 0u;
+            }
+            uint32_t etot;
+            uint32_t erank = tie_run + ex_scan(ne, wsum, etot);        // ties before this thread's
+            uint32_t na = 0;
+            bool adm[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                adm[q] = gt[q] || (eq[q] && erank < krem);
+                erank += eq[q] ? 1u : 0u;
+                na += adm[q] ? 1u : 0u;
+            }
+            uint32_t atot;
+            uint32_t pos = base + ex_scan(na, wsum, atot);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (adm[q]) { oi[pos] = (uint32_t)(j0 + q); ov[pos] = v[q]; ++pos; }
+            if (t == 0) ws.tab[c * n + row] = make_uint2(base, atot);
+            base += atot;
+            tie_run += etot;
+        }
+        if (t == 0) {
+            ws.thr[row] = thr;
+            ws.krem[row] = krem;
+            ws.rowcnt[row * RCS] = base;
+            ws.flags[row] = F_EXACT;
+        }
+        __syncthreads();
+    }
+}
+
 // Exact path, ambiguous ties: per chunk count of key == thr, then the exclusive prefix over
 // chunks (in index order) per row.  RowSrc without F_TIES get tieprefix = 0 (krem admits all ties).
 __global__ __launch_bounds__(256) void k_tie_count(RowSrc rows, int64_t n, int64_t d, SelWs ws) {
@@ -1741,8 +1871,8 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             FLC_CHECK_LAUNCH("k_randk_fine");
         }
     } else {  // TOPK
-        FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const bool dense_k = K * 16 > d;   // large K: the candidate list would not be smaller than the row
+        if (dense_k) FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const int64_t bpr = (C + 3) / 4;
         if (!dense_k) {
             { ProfScope _ps("k_topk_sample", st);
@@ -1764,8 +1894,16 @@ if (n < 128) hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(102
         } else {
             FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
         }
-        // exact path for failed rows (all rows when dense_k)
-        hipLaunchKernelGGL(k_build_worklist, dim3(1), dim3(1024), 0, st, n, K, d, ws, dense_k ? 1 : 0);
+        if (!dense_k) {
+            // rows the fast path failed (rare): exact selection, one launch
+            ProfScope _ps("k_topk_exact_rows", st);
+            const int eb = grid_stride_blocks(n, 2048);
+            if (vec) hipLaunchKernelGGL((k_topk_exact_rows<true>), dim3(eb), dim3(EX_NT), 0, st, rows, n, d, K, ws);
+            else hipLaunchKernelGGL((k_topk_exact_rows<false>), dim3(eb), dim3(EX_NT), 0, st, rows, n, d, K, ws);
+            FLC_CHECK_LAUNCH("k_topk_exact_rows");
+        } else {
+        // dense K: every row takes the exact multi-launch path
+        hipLaunchKernelGGL(k_build_worklist, dim3(1), dim3(1024), 0, st, n, K, d, ws, 1);
         FLC_CHECK_LAUNCH("k_build_worklist");
         const int64_t hb = (d + 65535) / 65536;
         for (int p = 0; p < 3; ++p) {
@@ -1784,6 +1922,7 @@ hipLaunchKernelGGL((k_radix_hist<true>), dim3(grid_stride_blocks(n * hb)), dim3(
 if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0, st, rows, n, d, ws);
         else hipLaunchKernelGGL((k_topk_filter<true, false>), dim3(gb), dim3(256), 0, st, rows, n, d, ws); }
         FLC_CHECK_LAUNCH("k_topk_filter(exact)");
+        }
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.

@@ -563,3 +563,27 @@ def test_weighted_fold_vs_reference(ag):
         got = body(Buf(), len(w), None, torch.from_numpy(x.copy()), H)
         assert got.device.type == "cpu"
         assert_bitexact(got, want)
+
+
+@pytest.mark.parametrize("kind", ["ties", "clustered"])
+def test_topk_exact_rows_unaligned(ag, kind):
+    """Rows the fast path fails (massive ties / a misjudging sample) go through the one-launch exact
+    selection (k_topk_exact_rows); rows given as pointers at 4-byte (not 16-byte) offsets take its
+    scalar loads.  Bit-exact against the oracle, fused fold and single-row compressVector."""
+    n, d, k = 3, 70001, 700
+    g = np.random.default_rng([d, k, 7])
+    rows = _topk_rows(kind, n, d, g)
+    enc = []
+    for i in range(n):
+        out = np.zeros(d, dtype=np.float32)
+        ind = oc.topk_indices(rows[i], k)
+        out[ind] = rows[i][ind]
+        enc.append(out)
+    want = oc.reduce_plain(enc)
+    flat = torch.zeros(n * d + 1, dtype=torch.float32, device="cuda")
+    flat[1:] = torch.from_numpy(rows.reshape(-1)).cuda()
+    views = [flat[1 + i * d: 1 + (i + 1) * d] for i in range(n)]
+    red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
+    assert_bitexact(red(views), want)
+    c = ag.initCompressor(f"topk:{k}", d)
+    assert_bitexact(c.compressVector(views[1]), enc[1])
