@@ -1125,6 +1125,7 @@ __device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64
         const uint32_t f = ws.flags[r];
         m.mode = (f & F_EXACT) ? 2u : ((f & F_TIES) ? 1u : 0u);
         if (m.mode == 1u) m.cut = ws.tiecut[r];
+        if (m.mode == 2u) m.thr = 0u;          // exact list: every entry admitted (key >= 0, cut ~0)
         if (w) m.w = w[r];
     }
     return m;
@@ -1227,10 +1228,14 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
                 rv[slot][h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dv, lane * 4, h * 256, 0));
             }
         };
+        // admission (key > T, or key == T and ix <= cut; load_meta folds the exact mode into
+        // T = 0, cut = ~0) as ONE 64-bit compare: (key, ~ix) >= (T, ~cut)
         auto fold = [&](uint32_t ix, float vv, uint32_t T, uint32_t cut, uint32_t mode, float wi) {
+            (void)mode;
             const uint32_t loc = ix - cbase;                   // ~0 index / other part: loc >= TS
-            const uint32_t key = mag_key(vv);
-            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut))) {
+            const uint64_t a = ((uint64_t)mag_key(vv) << 32) | (uint64_t)(~ix);
+            const uint64_t b = ((uint64_t)T << 32) | (uint64_t)(~cut);
+            if (loc < (uint32_t)TS && a >= b) {
                 if (ASSIGN) tl[loc] = vv;
                 else tl[loc] = W ? tl[loc] + wi * vv : tl[loc] + vv;
             }
@@ -1247,10 +1252,11 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
                     const int slot = q % AP;
                     const uint32_t T = __builtin_amdgcn_readlane(cur.thr, q);
                     const uint32_t cut = __builtin_amdgcn_readlane(cur.cut, q);
-                    const uint32_t mode = __builtin_amdgcn_readlane(cur.mode, q);
+                    const uint32_t mode = 0u;
                     const float wi = W ? __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(cur.w), q)) : 1.f;
                     fold(ri[slot][0], rv[slot][0], T, cut, mode, wi);
-                    fold(ri[slot][1], rv[slot][1], T, cut, mode, wi);
+                    // the second slot holds entries only when the list is longer than 64
+                    if (__builtin_amdgcn_readlane(cur.te.y, q) > 64u) fold(ri[slot][1], rv[slot][1], T, cut, mode, wi);
                     if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, slot);
                     else fetch(nxt, q + AP - 64, i0 + q + AP, slot);   // past n: empty lists
                 }
