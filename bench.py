@@ -420,6 +420,7 @@ def main():
     ap.add_argument("--n", "--clients", dest="n", type=int, default=None, help="override clients per GPU")
     ap.add_argument("--d", "--dim", dest="d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-counts-overlap", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--shift", choices=["diana", "ef21", "marina"], default=None,
                     help="the compressed algorithms' client step on one row (flc_encode_shift) vs torch ops")
     ap.add_argument("--step-times", action="store_true", help="per-step times (HIP events) on stderr")
@@ -554,6 +555,8 @@ def main():
     if mixed:
         row_list = [rows[i % n_dist] for i in range(n)]
         up = ag.MixedUplink(specs, d, seed=20241015, device=dev)
+        if args.no_counts_overlap:
+            up.counts_groups = []            # A/B: the RandK counts inside the call, not beside the filters
         group = None
         if world > 1:
             group = dist.group.WORLD

@@ -66,6 +66,7 @@ class FlcPattern(ctypes.Structure):
         ("client0", ctypes.c_int64),
         ("uniforms_ld", ctypes.c_int64),
         ("idx_ld", ctypes.c_int64),
+        ("d_randk_counts", ctypes.c_void_p),
     ]
 
 

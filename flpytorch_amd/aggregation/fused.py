@@ -41,20 +41,43 @@ class UplinkReducer:
         prm, _ = self.params()
         return _lib.load().flc_encode_reduce_workspace_size(ctypes.byref(prm), n, d)
 
+    def randk_counts(self, n, d, client0=0, out=None):
+        """The device sampler's chunk counts [ceil(d / 4096), n] (uint32 as int32) of clients
+        client0.. on the current stream (flc_device_randk_counts) — pure compute, no row is read;
+        hand them to __call__(randk_counts=...) to take that work out of the call."""
+        lib = _lib.load()
+        dev = self.device
+        if self.seed is None:
+            raise ValueError("device-RNG counts need a seed")
+        C = (d + 4095) // 4096
+        if out is None:
+            out = torch.empty((C, n), dtype=torch.int32, device=dev)
+        wsb = lib.flc_device_randk_counts_workspace_size(n, d)
+        if getattr(self, "_cnt_ws", None) is None or self._cnt_ws.numel() < wsb:
+            self._cnt_ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.flc_device_randk_counts(int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(client0), n, d, self.comp.K,
+                                             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self._cnt_ws.data_ptr()),
+                                             self._cnt_ws.numel(), _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_device_randk_counts")
+        return out
+
     def __call__(self, rows, out=None, weights=None, client0=0, randk_idx=None, uniforms=None, lazy_u=None,
-                 pnorms_out=None, stream=None, divisor=None):
+                 pnorms_out=None, stream=None, divisor=None, randk_counts=None):
         """rows: [N, D] fp32 device tensor (row stride % 4 == 0 for the vector path) or a list of
         [D] device tensors.  Compat patterns: randk_idx [N, K] int64, uniforms [N, D] float64,
         lazy_u [N] float64 (device).  Without them (and with ``seed`` set) draws are on device.
         ``divisor`` overrides the fp32 divisor sum(w) (e.g. 1.0 for a partial sum across GPUs).
         ``stream``: every allocation, copy and the launch go to that stream (torch's stream
-        semantics: the caller orders it after the producers of ``rows`` and the patterns)."""
+        semantics: the caller orders it after the producers of ``rows`` and the patterns).
+        ``randk_counts``: RandK device mode, the chunk counts from ``randk_counts(n, d, client0)``."""
         if stream is not None:
             with torch.cuda.stream(stream):
-                return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor)
-        return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor)
+                return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor,
+                                 randk_counts)
+        return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor, randk_counts)
 
-    def _run(self, rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor):
+    def _run(self, rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor, randk_counts=None):
         """The call on the current stream (allocations, uploads and the launch all on it)."""
         lib = _lib.load()
         dev = self.device
@@ -85,6 +108,10 @@ class UplinkReducer:
         if t == CompressorType.RANDK_COMPRESSOR and randk_idx is not None:
             pat.d_randk_idx = randk_idx.data_ptr()
             pat.idx_ld = randk_idx.stride(0)
+        if randk_counts is not None and t == CompressorType.RANDK_COMPRESSOR and randk_idx is None:
+            if tuple(randk_counts.shape) != ((d + 4095) // 4096, n) or not randk_counts.is_cuda:
+                raise ValueError("randk_counts must be a [ceil(d / 4096), n] device tensor")
+            pat.d_randk_counts = randk_counts.data_ptr()
         if uniforms is not None:
             pat.d_uniforms = uniforms.data_ptr()
             pat.uniforms_ld = uniforms.stride(0)

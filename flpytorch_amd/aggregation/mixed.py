@@ -15,6 +15,12 @@ number i // G, so every (codec, client) pair has its own stream.
 Multi-GPU: with a process group, each group's [D] partial is all-reduced (RCCL over xGMI) as soon
 as it is encoded, asynchronously, so the collective of group g overlaps the encode of group g+1
 (the sum is linear: allreduce(sum_g P_g) = sum_g allreduce(P_g)).
+
+RandK groups (HIP path, device draws): their chunk counts (k_randk_counts — the device sampler,
+pure compute, no HBM traffic) are computed on a side stream at the start of the call, under the
+other groups' streaming filters, and the RandK groups are encoded last from those counts.  Only
+the counts overlap: the RandK fold's gathers beside a filter measured 20x slower.  The partials
+land in separate buffers and are combined in group order, so the bits do not depend on this.
 """
 import torch
 
@@ -40,12 +46,20 @@ class MixedUplink:
                         for sp, sd in zip(self.specs, self.seeds)]
             self.device = reducers[0].device
 
-            def encode_partial(g, rows_g, c0, out):
-                reducers[g](rows_g, out=out, client0=c0, divisor=1.0)
+            def encode_partial(g, rows_g, c0, out, counts=None):
+                reducers[g](rows_g, out=out, client0=c0, divisor=1.0, randk_counts=counts)
+
+            def counts_of(g, n_g, c0, out=None):
+                return reducers[g].randk_counts(n_g, D, c0, out=out)
+            self.counts_of = counts_of
+            self.counts_groups = [g for g, sp in enumerate(self.specs) if sp.split(":")[0] == "randk"]
         else:
             self.device = torch.device(device) if device is not None else torch.device("cpu")
+            self.counts_groups = []
         self.encode_partial = encode_partial
         self._parts = None
+        self._side = None
+        self._counts = {}
 
     def groups(self, client0, n):
         """Positions (0..n-1) of the clients client0..client0+n-1 in each codec group, and the client
@@ -62,13 +76,45 @@ class MixedUplink:
             self._parts = torch.empty((self.G, self.D), dtype=torch.float32, device=self.device)
         parts = self._parts
         handles = []
-        for g, (pos, c0) in enumerate(self.groups(client0, n)):
+        grouped = self.groups(client0, n)
+        early = [g for g in self.counts_groups if grouped[g][0]]
+        counts = {}
+        if early and len(early) < self.G:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            main = torch.cuda.current_stream(self.device)
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                for g in early:
+                    pos, c0 = grouped[g]
+                    buf = self._counts.get(g)
+                    if buf is None or buf.shape[1] != len(pos):
+                        buf = self._counts[g] = None
+                    counts[g] = self._counts[g] = self.counts_of(g, len(pos), c0, out=buf)
+            self._counts_ready = torch.cuda.Event()
+            self._counts_ready.record(self._side)
+        else:
+            early = []
+
+        def run(g):
+            pos, c0 = grouped[g]
             if pos:
-                self.encode_partial(g, [rows[i] for i in pos], c0, parts[g])
+                if g in counts:
+                    self.encode_partial(g, [rows[i] for i in pos], c0, parts[g], counts[g])
+                else:
+                    self.encode_partial(g, [rows[i] for i in pos], c0, parts[g])
             else:
                 parts[g].zero_()
             if group is not None:
                 handles.append(torch.distributed.all_reduce(parts[g], group=group, async_op=True))
+
+        for g in range(self.G):
+            if g not in early:
+                run(g)
+        if early:
+            torch.cuda.current_stream(self.device).wait_event(self._counts_ready)
+            for g in early:
+                run(g)
         return parts, handles
 
     def __call__(self, rows, client0=0, total_weight=None, out=None, group=None):

@@ -1327,6 +1327,12 @@ struct RkdWs {
 constexpr int RKC_NT = 1024;
 constexpr int64_t RKC_BINS = 32768;
 
+// the client keys of the device sampler (k_randk_counts writes them beside the counts)
+__global__ __launch_bounds__(256) void k_randk_ckeys(int64_t n, uint64_t seed, int64_t client0, uint64_t* __restrict__ ckey) {
+    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (row < n) ckey[row] = client_key(seed, client0 + row);
+}
+
 __global__ __launch_bounds__(RKC_NT) void k_randk_counts(int64_t n, int64_t d, int64_t K, uint64_t seed, int64_t client0,
                                                          RkdWs ws) {
     __shared__ uint32_t bins[RKC_BINS / 2];
@@ -1775,15 +1781,14 @@ int randk_device_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, in
                         size_t ws_bytes, hipStream_t st) {
     if (ws_bytes < randk_device_workspace(n, d)) { set_error("randk counts: workspace too small"); return FLC_ERR_WORKSPACE; }
     RkdWs ws = carve_rkd(wsp, n, d, nullptr);
+    ws.cnt = cnt;                                    // the counts straight into the caller's array
     flc_codec_params prm{};
     prm.codec = FLC_RANDK;
     prm.k = k;
     prm.seed = seed;
     flc_pattern pat{};
     pat.client0 = client0;
-    if (int rc = randk_counts(&prm, &pat, n, d, ws, st)) return rc;
-    FLC_CHECK_HIP(hipMemcpyAsync(cnt, ws.cnt, (size_t)host_chunks(d) * n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    return FLC_OK;
+    return randk_counts(&prm, &pat, n, d, ws, st);
 }
 
 // device-RNG RandK encode + reduce: counts, then the list-free chunk fold
@@ -1799,8 +1804,20 @@ int randk_device_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc
     // wave regenerating the rows' members of its chunk.  Short rows: too few chunks for the
     // row-serial fold, so the members are written per row (k_randk_gen) and the chunk fold runs
     // over the lists with its column split (k_chunk_accum).
+    // chunk counts: the caller's (flc_pattern.d_randk_counts, made by flc_device_randk_counts) or
+    // computed here; the client keys are cheap and always computed here
+    auto counts = [&]() -> int {
+        if (pat && pat->d_randk_counts) {
+            rw.cnt = const_cast<uint32_t*>(pat->d_randk_counts);          // read only below
+            hipLaunchKernelGGL(k_randk_ckeys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, prm->seed,
+                               pat->client0, rw.ckey);
+            FLC_CHECK_LAUNCH("k_randk_ckeys");
+            return FLC_OK;
+        }
+        return randk_counts(prm, pat, n, d, rw, st);
+    };
     if (C >= 1024) {
-        if (int rc = randk_counts(prm, pat, n, d, rw, st)) return rc;
+        if (int rc = counts()) return rc;
         ProfScope _ps("k_randk_fold", st);
         const int ab = grid_stride_blocks((C + 3) / 4, 16384);
         hipLaunchKernelGGL((k_randk_fold<CHUNK>), dim3(ab), dim3(256), 0, st, rows, n, d, rw.cnt, rw.ckey,
@@ -1808,7 +1825,7 @@ int randk_device_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc
         FLC_CHECK_LAUNCH("k_randk_fold");
         return FLC_OK;
     }
-    if (int rc = randk_counts(prm, pat, n, d, rw, st)) return rc;
+    if (int rc = counts()) return rc;
     hipLaunchKernelGGL(k_randk_tab, dim3((unsigned)n), dim3(256), 0, st, n, d, prm->k, rw.cnt, sw);
     FLC_CHECK_LAUNCH("k_randk_tab");
     {

@@ -91,6 +91,10 @@ typedef struct {
     int64_t client0;            /* device mode: id of row 0 (row r is client client0 + r) */
     int64_t uniforms_ld;        /* leading dimension of d_uniforms (elements); 0 = d */
     int64_t idx_ld;             /* leading dimension of d_randk_idx (elements); 0 = k */
+    const uint32_t* d_randk_counts; /* randk device mode: the rows' chunk counts [ceil(d/4096)][n]
+                                   * from flc_device_randk_counts with the same seed, client0, n, d,
+                                   * k (e.g. computed on another stream, beside other work), or
+                                   * NULL: computed inside the call */
 } flc_pattern;
 
 /* ----------------------------------------------------------------------------------------

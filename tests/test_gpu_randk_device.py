@@ -120,3 +120,23 @@ def test_device_randk_compress_vector(ag, d, spec):
     o = oc.OracleCompressor(spec, d)
     o.S = devrng.randk_indices(seed, client, d, o.K)
     assert np.array_equal(bits(got), bits(o.compress(x)))
+
+
+@pytest.mark.parametrize("n,d,spec", [(3, 100_003, "randk:1%"), (2, 5_000_003, "randk:1%"), (70, 40_000, "randk:1%")])
+def test_device_randk_precomputed_counts(ag, n, d, spec):
+    """flc_pattern.d_randk_counts: counts made ahead by flc_device_randk_counts on another stream
+    (how MixedUplink overlaps them) give the same bits as the counts made inside the call, on both
+    the short-row (lists) and the long-row (list-free fold) paths."""
+    seed, client0 = 777, 5
+    rows = np.random.default_rng([n, d, 1]).standard_normal((n, d)).astype(np.float32)
+    want = oracle_fold(rows, spec, seed, client0)
+    red = ag.UplinkReducer(ag.initCompressor(spec, d), seed=seed)
+    rt = torch.from_numpy(rows).cuda()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        cnt = red.randk_counts(n, d, client0)
+    torch.cuda.current_stream().wait_stream(side)
+    got = red(rt, client0=client0, randk_counts=cnt).cpu().numpy()
+    assert np.array_equal(bits(got), bits(want))
+    assert int(cnt.sum()) == n * red.comp.K
