@@ -55,6 +55,9 @@
 namespace flc {
 
 constexpr uint32_t DS_DENSE = 1u, DS_FAST = 4u;
+#ifndef FLC_DS_W2
+#define FLC_DS_W2 1
+#endif
 constexpr int DS_FGS = 2;                  // chunks per filter work item (8192 elements)
 constexpr int DS_NH = 2 * DS_FGS;          // fold tiles (half chunks) per item
 constexpr int DS_GCAP = 512;               // staged candidates per item (6.25 %; more -> row overflow)
@@ -212,6 +215,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
     uint2* sg = stage[wv];
     uint16_t* s16 = stage16[wv];
+    // LDS byte address of the wave's staging buffer (wave-uniform)
+    const uint32_t sla = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint2*)sg);
     float4 ring[RING];
     // item order: blocks of rb rows (the last one shorter), and inside a block (gi, row) with the
     // row fastest: the waves in flight at any time read the same item of the block's rows, spread
@@ -284,14 +289,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     // is dropped; NaN from 0 * inf (qc = inf) is not a candidate
                     const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
                     const uint64_t m = __ballot(f);
-                    // position = cnt + candidates in lower lanes; an item past GCAP overflows (its
-                    // row is folded dense), so wrapping is harmless
-                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
                     // exec-masked store (a branch-free store of every element to a per-lane spill
                     // slot measured 9.2 -> 11.9 ms: the staging is LDS-issue sensitive)
                     if (PROBE != 2 && f) {
+#if FLC_DS_W2
+                        // slot = min(cnt, GCAP - 64) + candidates in lower lanes: the scalar part
+                        // is folded into the wave's LDS address in SALU (sla), the lane part is one
+                        // mbcnt pair; an item past GCAP overflows (its row is folded dense), so
+                        // its last 64 slots being overwritten is harmless.  Index and x go out as
+                        // one ds_write2_b32 (no register pair to assemble for a 64-bit store).
+                        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        uint32_t sb = sla + min(cnt, (uint32_t)(GCAP - 64)) * 8u;
+                        asm volatile("" : "+s"(sb));             // stays a scalar term: one v_lshl_add
+                        const uint32_t la = sb + pre * 8u;
+                        asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(jb + (uint32_t)(L * 256 + q)),
+                                     "v"(__float_as_uint(vq[q])) : "memory");
+#else
+                        const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
                         sg[pos] = make_uint2(jb + (uint32_t)(L * 256 + q), __float_as_uint(vq[q]));
+#endif
                     }
                     cnt += (uint32_t)__popcll(m);
                 }

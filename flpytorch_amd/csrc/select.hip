@@ -459,8 +459,8 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 template <int RING, int FGS>
 __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
-    __shared__ uint32_t st_idx[2][4][GCAP];
-    __shared__ float st_val[2][4][GCAP];
+    // staging per (buffer, wave): GCAP indices then GCAP values (one ds_write2st64_b32 per entry)
+    __shared__ uint32_t st[2][4][2 * GCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
     const int64_t C = nchunks(d);
@@ -512,8 +512,8 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
         }
         if (!fits && lane == 0) atomicOr(&ws.flags[prow], F_OVERFLOW);
         if (fits) {
-            const uint32_t* si = st_idx[pb][wv];
-            const float* sv = st_val[pb][wv];
+            const uint32_t* si = st[pb][wv];
+            const float* sv = reinterpret_cast<const float*>(st[pb][wv] + GCAP);
             uint32_t* oi = ws.ent_idx + prow * ws.cap + base;
             float* ov = ws.ent_val + prow * ws.cap + base;
             // fixed trip count (GCAP / 64 predicated slots): the compiler's vmcnt bookkeeping
@@ -528,8 +528,8 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
     while (it < items) {
         const uint32_t T = sload(ws.thr + row);
         const int64_t nit = it + stride;
-        uint32_t* si = st_idx[par][wv];
-        float* sv = st_val[par][wv];
+        // LDS byte address of this group's staging (wave-uniform)
+        const uint32_t sla = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)st[par][wv]);
         uint32_t cnt = 0;                    // entries in this group so far
         uint64_t ccp = 0;
         const int64_t cg0 = c;
@@ -567,12 +567,18 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
                 for (int q = 0; q < 4; ++q) {
                     const bool f = (jl + q < lim) && mag_key(vq[q]) >= T;
                     const uint64_t m = __ballot(f);
-                    if (m) {
-                        const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt));
-                        if (f && pos < GCAP) { si[pos] = (uint32_t)j0 + jl + q; sv[pos] = vq[q]; }
-                        cnt += (uint32_t)__popcll(m);
+                    if (f) {
+                        // slot = min(cnt, GCAP - 64) + entries in lower lanes (a group past GCAP
+                        // overflows and its row takes the exact path, so overwritten last slots
+                        // are harmless); the scalar part folded into the LDS address in SALU, the
+                        // index and value out as one ds_write2st64_b32 (values GCAP words on)
+                        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        uint32_t sb = sla + min(cnt, (uint32_t)(GCAP - 64)) * 4u;
+                        asm volatile("" : "+s"(sb));
+                        asm volatile("ds_write2st64_b32 %0, %1, %2 offset1:%3" ::"v"(sb + pre * 4u),
+                                     "v"((uint32_t)j0 + jl + q), "v"(__float_as_uint(vq[q])), "i"(GCAP * 4 / 256) : "memory");
                     }
+                    cnt += (uint32_t)__popcll(m);
                 }
             }
             ccp |= (uint64_t)min(cnt - cnt0, 0xFFFFu) << (16 * (c - cg0));
