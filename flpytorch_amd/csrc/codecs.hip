@@ -109,9 +109,22 @@ __global__ __launch_bounds__(64) void k_norm_final(const double* __restrict__ pa
     if (row >= n) return;
     double a = 0.0;
     uint32_t tiny = 0;
-    for (int64_t p = threadIdx.x; p < parts; p += 64) {
-        a = ncomb<NORM>(a, partial[row * parts + p]);
-        tiny |= tinyp[row * parts + p];
+    // lane t combines partials t, t + 64, ... in that order; 8 of them loaded per round trip (the
+    // partials come from every XCD: each load is a far miss, thousands of them for a lone row)
+    const double* pr = partial + row * parts;
+    const uint32_t* tr = tinyp + row * parts;
+    int64_t p = threadIdx.x;
+    for (; p + 7 * 64 < parts; p += 8 * 64) {
+        double v[8];
+        uint32_t t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { v[u] = pr[p + u * 64]; t[u] = tr[p + u * 64]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { a = ncomb<NORM>(a, v[u]); tiny |= t[u]; }
+    }
+    for (; p < parts; p += 64) {
+        a = ncomb<NORM>(a, pr[p]);
+        tiny |= tr[p];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

@@ -428,7 +428,16 @@ __global__ __launch_bounds__(256) void k_ds_final(int64_t r0, int64_t rn, DsWs w
     if (row >= r0 + rn) return;
     double a = 0.0;
     uint32_t ov = 0;
-    for (int64_t k = lane; k < ws.G; k += 64) { a += ws.partial[row * ws.G + k]; ov |= ws.itm[k * ws.n + row] == DS_OVF; }
+    int64_t k = lane;
+    for (; k + 7 * 64 < ws.G; k += 8 * 64) {                 // 8 far loads per round trip, same order
+        double v[8];
+        uint32_t t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { v[u] = ws.partial[row * ws.G + k + u * 64]; t[u] = ws.itm[(k + u * 64) * ws.n + row]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { a += v[u]; ov |= t[u] == DS_OVF; }
+    }
+    for (; k < ws.G; k += 64) { a += ws.partial[row * ws.G + k]; ov |= ws.itm[k * ws.n + row] == DS_OVF; }
     a = wave_sum(a);
     ov = __ballot(ov != 0u) != 0ull;
     if (lane == 0) {
