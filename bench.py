@@ -421,6 +421,8 @@ def main():
     ap.add_argument("--d", "--dim", dest="d", type=int, default=None, help="override D")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counts-overlap", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist", choices=["normal", "heavy"], default="normal",
+                    help="synthetic rows: N(0,1) (default) or N(0,1) * 10^U(-3,3) (SURVEY 8d)")
     ap.add_argument("--shift", choices=["diana", "ef21", "marina"], default=None,
                     help="the compressed algorithms' client step on one row (flc_encode_shift) vs torch ops")
     ap.add_argument("--step-times", action="store_true", help="per-step times (HIP events) on stderr")
@@ -508,6 +510,12 @@ def main():
     rows = torch.empty((n_dist, d), dtype=torch.float32, device=dev)
     for i in range(0, n_dist, 64):
         rows[i:i + 64].normal_(generator=gen)
+        if args.dist == "heavy":
+            # SURVEY §8d's second distribution: N(0,1) * 10^U(-3,3), a wide dynamic range that moves
+            # the TopK thresholds and the QSGD level mix (heavy-tailed norm samples)
+            e = torch.empty_like(rows[i:i + 64]).uniform_(-3.0, 3.0, generator=gen)
+            rows[i:i + 64].mul_(torch.pow(10.0, e))
+            del e
     out = torch.empty(d, dtype=torch.float32, device=dev)
     client0 = rank * n
     compat_kw, compat_bytes, compat_note = {}, 0, None
@@ -684,7 +692,8 @@ def main():
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic N(0,1) fp32 rows generated on device (seeded per rank); "
+            "data": ("synthetic N(0,1) * 10^U(-3,3)" if args.dist == "heavy" else "synthetic N(0,1)")
+                    + " fp32 rows generated on device (seeded per rank); "
                     + (f"compat patterns (the reference's numpy stream, resident in HBM; {compat_note})"
                        if args.compat else "device-RNG patterns")
                     + (f"; {n_dist} resident distinct rows replayed through the {n} clients' row pointers, "
