@@ -526,7 +526,10 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
         }
     };
     while (it < items) {
-        const uint32_t T = sload(ws.thr + row);
+        // key >= max(T, 1): the loads past the row end return +0 (key 0), so no per-element range
+        // test; a row whose K-th magnitude is 0 (fewer than K nonzeros) comes up short and takes
+        // the exact path, which admits zeros
+        const uint32_t T = max(sload(ws.thr + row), 1u);
         const int64_t nit = it + stride;
         // LDS byte address of this group's staging (wave-uniform)
         const uint32_t sla = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)st[par][wv]);
@@ -535,12 +538,11 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
         const int64_t cg0 = c;
         int64_t nrow = row, nc = c;
         // straight-line over the group, no early exit: the chunks of a row's short last group
-        // past the row end have lim 0 and empty descriptors (their loads return zeros), so the
+        // past the row end have empty descriptors (their loads return zeros), so the
         // compiler's vmcnt bookkeeping stays exact from one group's atomic to its use
 #pragma unroll
         for (int sub = 0; sub < FGS; ++sub, ++c) {
             const int64_t j0 = c * CHUNK;
-            const uint32_t lim = (uint32_t)max((int64_t)0, min((int64_t)CHUNK, d - j0));  // valid elements
             // descriptor of the chunk after this one (same group, else the next item's first)
             __amdgpu_buffer_rsrc_t rsn;
             if (sub + 1 < FGS) {
@@ -554,18 +556,18 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
             const uint32_t cnt0 = cnt;
             // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
             // component) index constants out of the loop into 64 live VGPRs
-            uint32_t lb = (uint32_t)lane * 4u;
+            uint32_t lb = (uint32_t)j0 + (uint32_t)lane * 4u;   // row index of the lane's element 0
             asm volatile("" : "+v"(lb));
 #pragma unroll
             for (int L = 0; L < 16; ++L) {
                 const int P = L + RING - 1;
                 ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
                 const float4 x = ring[L % RING];
-                const uint32_t jl = lb + (uint32_t)(L * 256);             // offset inside the chunk
+                const uint32_t jl = lb + (uint32_t)(L * 256);             // index in the row
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const bool f = (jl + q < lim) && mag_key(vq[q]) >= T;
+                    const bool f = mag_key(vq[q]) >= T;
                     const uint64_t m = __ballot(f);
                     if (f) {
                         // slot = min(cnt, GCAP - 64) + entries in lower lanes (a group past GCAP
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
                         uint32_t sb = sla + min(cnt, (uint32_t)(GCAP - 64)) * 4u;
                         asm volatile("" : "+s"(sb));
                         asm volatile("ds_write2st64_b32 %0, %1, %2 offset1:%3" ::"v"(sb + pre * 4u),
-                                     "v"((uint32_t)j0 + jl + q), "v"(__float_as_uint(vq[q])), "i"(GCAP * 4 / 256) : "memory");
+                                     "v"(jl + q), "v"(__float_as_uint(vq[q])), "i"(GCAP * 4 / 256) : "memory");
                     }
                     cnt += (uint32_t)__popcll(m);
                 }

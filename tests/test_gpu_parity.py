@@ -242,6 +242,11 @@ def _topk_rows(kind, n, d, g):
         r = (g.standard_normal((n, d)) * 1e-3).astype(np.float32)
         r[:, d // 3: d // 3 + d // 50] *= 1e4
         return r
+    if kind == "fewnz":              # fewer than K nonzeros: the K-th magnitude is 0 (zeros admitted)
+        r = np.zeros((n, d), dtype=np.float32)
+        r[:, ::97] = g.standard_normal((n, len(range(0, d, 97)))).astype(np.float32)
+        r[:, ::3 * 97] = 0.0
+        return r
     if kind == "nan_inf":
         r = g.standard_normal((n, d)).astype(np.float32)
         r[:, 5] = np.inf
@@ -250,7 +255,7 @@ def _topk_rows(kind, n, d, g):
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["normal", "ties", "zeros", "clustered", "nan_inf"])
+@pytest.mark.parametrize("kind", ["normal", "ties", "zeros", "clustered", "nan_inf", "fewnz"])
 @pytest.mark.parametrize("n,d,k", [(3, 4096, 41), (4, 100003, 1000), (2, 1 << 20, 10486), (3, 50000, 20000)])
 def test_topk_vs_oracle(ag, kind, n, d, k):
     g = np.random.default_rng([d, k])
