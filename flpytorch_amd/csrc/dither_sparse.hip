@@ -203,7 +203,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     static_assert(GCAP % 512 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
     constexpr int DS_ITEM_STORES = 4 + GCAP / 128;   // partial, itm, tab, sure and ambiguous copy-outs
-    __shared__ uint2 stage[4][GCAP];                         // (entry word, x bits)
+    // (entry word, x bits); 64 slots past GCAP take the writes of a wave-instruction that starts
+    // at GCAP (its item has overflowed)
+    __shared__ uint2 stage[4][GCAP + 64];
     __shared__ __attribute__((aligned(16))) uint16_t stage16[4][GCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -293,13 +295,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     // slot measured 9.2 -> 11.9 ms: the staging is LDS-issue sensitive)
                     if (PROBE != 2 && f) {
 #if FLC_DS_W2
-                        // slot = min(cnt, GCAP - 64) + candidates in lower lanes: the scalar part
-                        // is folded into the wave's LDS address in SALU (sla), the lane part is one
-                        // mbcnt pair; an item past GCAP overflows (its row is folded dense), so
-                        // its last 64 slots being overwritten is harmless.  Index and x go out as
-                        // one ds_write2_b32 (no register pair to assemble for a 64-bit store).
+                        // slot = min(cnt, GCAP) + candidates in lower lanes (< GCAP + 64): exact
+                        // while the item fits; past GCAP the item overflows (its row is folded
+                        // dense) and the writes land in the spare slots.  The scalar part is folded
+                        // into the wave's LDS address in SALU (sla), the lane part is one mbcnt
+                        // pair; index and x go out as one ds_write2_b32 (no register pair to
+                        // assemble for a 64-bit store).
                         const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        uint32_t sb = sla + min(cnt, (uint32_t)(GCAP - 64)) * 8u;
+                        uint32_t sb = sla + min(cnt, (uint32_t)GCAP) * 8u;
                         asm volatile("" : "+s"(sb));             // stays a scalar term: one v_lshl_add
                         const uint32_t la = sb + pre * 8u;
                         asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(jb + (uint32_t)(L * 256 + q)),

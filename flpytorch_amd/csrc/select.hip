@@ -459,8 +459,11 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 template <int RING, int FGS>
 __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
-    // staging per (buffer, wave): GCAP indices then GCAP values (one ds_write2st64_b32 per entry)
-    __shared__ uint32_t st[2][4][2 * GCAP];
+    // staging per (buffer, wave): GCAP + 64 indices then GCAP + 64 values (one ds_write2st64_b32
+    // per entry; the 64 spare slots take a wave-instruction starting at GCAP, i.e. an overflow)
+    constexpr int SROW = GCAP + 64;
+    static_assert((SROW * 4) % 256 == 0, "value block offset in 256-byte units");
+    __shared__ uint32_t st[2][4][2 * SROW];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
     const int64_t C = nchunks(d);
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
         if (!fits && lane == 0) atomicOr(&ws.flags[prow], F_OVERFLOW);
         if (fits) {
             const uint32_t* si = st[pb][wv];
-            const float* sv = reinterpret_cast<const float*>(st[pb][wv] + GCAP);
+            const float* sv = reinterpret_cast<const float*>(st[pb][wv] + SROW);
             uint32_t* oi = ws.ent_idx + prow * ws.cap + base;
             float* ov = ws.ent_val + prow * ws.cap + base;
             // fixed trip count (GCAP / 64 predicated slots): the compiler's vmcnt bookkeeping
@@ -570,15 +573,16 @@ __global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n
                     const bool f = mag_key(vq[q]) >= T;
                     const uint64_t m = __ballot(f);
                     if (f) {
-                        // slot = min(cnt, GCAP - 64) + entries in lower lanes (a group past GCAP
-                        // overflows and its row takes the exact path, so overwritten last slots
-                        // are harmless); the scalar part folded into the LDS address in SALU, the
-                        // index and value out as one ds_write2st64_b32 (values GCAP words on)
+                        // slot = min(cnt, GCAP) + entries in lower lanes (< GCAP + 64): exact while
+                        // the group fits; past GCAP it overflows (its row takes the exact path) and
+                        // the writes land in the spare slots.  The scalar part folded into the LDS
+                        // address in SALU, index and value out as one ds_write2st64_b32 (values
+                        // SROW words on)
                         const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        uint32_t sb = sla + min(cnt, (uint32_t)(GCAP - 64)) * 4u;
+                        uint32_t sb = sla + min(cnt, (uint32_t)GCAP) * 4u;
                         asm volatile("" : "+s"(sb));
                         asm volatile("ds_write2st64_b32 %0, %1, %2 offset1:%3" ::"v"(sb + pre * 4u),
-                                     "v"(jl + q), "v"(__float_as_uint(vq[q])), "i"(GCAP * 4 / 256) : "memory");
+                                     "v"(jl + q), "v"(__float_as_uint(vq[q])), "i"(SROW * 4 / 256) : "memory");
                     }
                     cnt += (uint32_t)__popcll(m);
                 }

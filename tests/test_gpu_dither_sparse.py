@@ -190,3 +190,23 @@ def test_auto_path_choice(ag, monkeypatch):
             assert _lib.profile_collect(other)[1] == 0, (d, other)
         finally:
             _lib.profile_enable(False)
+
+
+@pytest.mark.parametrize("big", [440, 470, 505, 530])
+def test_sparse_dither_item_near_staging_capacity(ag, monkeypatch, big):
+    """A filter item (8192 elements) whose candidate count lands just below, at and just past
+    its 512-entry LDS staging: `big` elements of the first item at +-1 (kept at a level >= 1 for
+    sure, so always candidates) plus ~1/256 of the small rest.  Below 512 the item's entries are
+    staged exactly (slot = running count + lane prefix); past it the row is folded dense."""
+    n, d, client0, spec = 3, 16384, 2, "qsgd:127"
+    g = np.random.default_rng(big)
+    rows = (g.standard_normal((n, d)) * 1e-3).astype(np.float32)
+    for i in range(n):
+        idx = g.choice(8192, size=big, replace=False)
+        rows[i, idx] = np.where(g.random(big) < 0.5, -1.0, 1.0).astype(np.float32)
+    want, wn = oracle_uplink(spec, rows, client0)
+    red = ag.UplinkReducer(sparse(ag, spec, d), seed=SEED)
+    pn = torch.empty(n, device="cuda")
+    got = red(torch.from_numpy(rows).cuda(), client0=client0, pnorms_out=pn)
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)

@@ -592,3 +592,26 @@ def test_topk_exact_rows_unaligned(ag, kind):
     assert_bitexact(red(views), want)
     c = ag.initCompressor(f"topk:{k}", d)
     assert_bitexact(c.compressVector(views[1]), enc[1])
+
+
+@pytest.mark.parametrize("k", [440, 490, 511, 512, 530])
+def test_topk_group_near_staging_capacity(ag, k):
+    """Every one of the top K magnitudes in the first filter group (2 chunks for small inputs):
+    its candidate count sits just below, at or past the 512-entry LDS staging (exact slots below,
+    the exact path past it).  D <= 16 K: the sample is the whole row, so the candidates are
+    exactly the top K."""
+    n, d = 3, 16384
+    g = np.random.default_rng(k)
+    rows = (g.standard_normal((n, d)) * 1e-3).astype(np.float32)
+    for i in range(n):
+        idx = g.choice(8192, size=k, replace=False)
+        rows[i, idx] = (g.standard_normal(k) * 10).astype(np.float32)
+    enc = []
+    for i in range(n):
+        out = np.zeros(d, dtype=np.float32)
+        ind = oc.topk_indices(rows[i], k)
+        out[ind] = rows[i][ind]
+        enc.append(out)
+    want = oc.reduce_plain(enc)
+    red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
+    assert_bitexact(red(torch.from_numpy(rows).cuda()), want)
