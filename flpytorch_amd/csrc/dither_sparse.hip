@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // 2048-element half chunk (the fold's tile).
 // ------------------------------------------------------------------------------------------
 // PROBE (tuning build only, FLC_DS_PROBE; outputs NOT valid): 1 fp32 norm; 2 no candidate staging;
-// 3 loads + norm only
+// 3 loads + norm only; 4 the draw's group hash without its multiplies
 template <int RING, int GCAP, int PROBE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws) {
     constexpr int FGS = DS_FGS, NH = DS_NH;
@@ -279,7 +279,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                 const int P = L + RING - 1;
                 ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
                 const float4 x = ring[L % RING];
-                const uint32_t hg = fmix32(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
+                uint32_t hg;
+                if (PROBE == 4) { hg = gb + (uint32_t)(L * 64) * 0x9E3779B1u; hg ^= hg >> 15; }   // cost probe only
+                else hg = fmix32(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -906,7 +908,8 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
 
     auto filter = [&](int64_t r0, int64_t rn) -> int {
         auto kern = v.probe == 1 ? k_ds_filter<16, DS_GCAP, 1> : v.probe == 2 ? k_ds_filter<16, DS_GCAP, 2>
-                  : v.probe == 3 ? k_ds_filter<16, DS_GCAP, 3> : k_ds_filter<16, DS_GCAP>;
+                  : v.probe == 3 ? k_ds_filter<16, DS_GCAP, 3> : v.probe == 4 ? k_ds_filter<16, DS_GCAP, 4>
+                  : k_ds_filter<16, DS_GCAP>;
         int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
         if (v.resident || (K > 1 && v.gridpct < 100)) {
             int per = 0, dev = 0, cus = 0;
