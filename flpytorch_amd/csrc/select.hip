@@ -1911,8 +1911,8 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         const int64_t bpr = (C + 3) / 4;
         if (!dense_k) {
             { ProfScope _ps("k_topk_sample", st);
-if (n < 128) hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws);
-            else hipLaunchKernelGGL(k_topk_sample<256>, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, K, ws); }
+            // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3)
+            hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             { ProfScope _ps("k_topk_filter", st);
             // persistent grid: exactly the resident blocks (a second partial wave of blocks would
@@ -1924,8 +1924,9 @@ if (n < 128) hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(102
             FLC_CHECK_LAUNCH("k_topk_filter");
             { ProfScope _ps("k_cand_select", st);
             // few rows (a lone compressVector): one 1024-thread workgroup per row walks the list 4x wider
+            // many rows: 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
             if (n < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)n), dim3(1024), 0, st, n, K, ws);
-            else hipLaunchKernelGGL(k_cand_select<256>, dim3(grid_stride_blocks(n, 8192)), dim3(256), 0, st, n, K, ws); }
+            else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(n, 8192)), dim3(512), 0, st, n, K, ws); }
             FLC_CHECK_LAUNCH("k_cand_select");
         } else {
             FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
