@@ -67,7 +67,10 @@ constexpr int DS_SMAX = 16384;             // sample elements per row
 constexpr float DS_QT = 254.98f;
 constexpr int DS_MAXS = 512;               // level table entries kept in LDS by the fold
 constexpr uint32_t DS_OVF = 0xFFFFFFFFu;   // itm: the item overflowed its staging capacity
-constexpr int DS_AP = 8;                   // rows of entry lists in flight in the fold
+#ifndef FLC_DS_AP
+#define FLC_DS_AP 16                // 16: measured 0.673 -> 0.622 ms at C4 (32: same as 16)
+#endif
+constexpr int DS_AP = FLC_DS_AP;           // rows of entry lists in flight in the fold
 // rows per block of the filter's item order: 16 measured as fast as one block of all rows at C4
 // (and 1, row-major, 1-2 % slower on the same box); a block never reads one row twice, so rows
 // that alias (C5's replayed pool) are still read from HBM once per client

@@ -1119,7 +1119,10 @@ __global__ __launch_bounds__(RK_FTHR) void k_randk_fine(RowSrc rows, int64_t n, 
 // flight while a row is folded (a ring of AP register slots, 2 x 64 entries per row), so the
 // wave never waits on a dependent tab -> entries round trip.
 // ------------------------------------------------------------------------------------------
-constexpr int AP = 8;                      // rows of entry lists in flight
+#ifndef FLC_CA_AP
+#define FLC_CA_AP 8
+#endif
+constexpr int AP = FLC_CA_AP;              // rows of entry lists in flight
 
 struct RowMeta {
     uint2 te;          // (offset, count) of the row's list in this chunk
