@@ -1542,6 +1542,10 @@ __device__ void rk_resolve_neg_zero(float* tl, uint32_t* rm, const uint32_t* cnt
     }
 }
 
+#ifndef FLC_RK_AP
+#define FLC_RK_AP 8
+#endif
+constexpr int RK_AP = FLC_RK_AP;
 template <int TS>
 __global__ __launch_bounds__(256) void k_randk_fold(RowSrc rows, int64_t n, int64_t d, const uint32_t* __restrict__ cnt,
                                                     const uint64_t* __restrict__ ckey, float scale,
@@ -1561,6 +1565,7 @@ __global__ __launch_bounds__(256) void k_randk_fold(RowSrc rows, int64_t n, int6
         const int64_t cbase = c * CHUNK;
         const uint32_t clen = (uint32_t)min((int64_t)CHUNK, d - cbase);
         for (int i = lane; i < TS; i += 64) tl[i] = -0.f;     // the additive identity
+        constexpr int AP = RK_AP;                             // rows in flight (their gathers)
         uint32_t ro[AP];                                      // ring: part-local column (>= TS: none)
         float rv[AP];                                         //       gathered x
         // row q of the current batch: its members' columns for this lane, one gather in flight
