@@ -4,7 +4,7 @@
 # traffic in separate passes.  Output under gpurun_out/ev4; copy what is judged into profiles/r02b.
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-out=gpurun_out/ev4
+out=gpurun_out/${EV_OUT:-ev4}
 mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
     --timeout-method thread -rf > $out/gpu_tests.log 2>&1 || exit $?
