@@ -201,7 +201,10 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // PROBE (tuning build only, FLC_DS_PROBE; outputs NOT valid): 1 fp32 norm; 2 no candidate staging;
 // 3 loads + norm only; 4 the draw's group hash without its multiplies
 template <int RING, int GCAP, int PROBE = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws) {
+#ifndef FLC_DS_WPE
+#define FLC_DS_WPE 6                 // 6 waves per SIMD (80 VGPRs): measured 9.19 -> 9.10 ms at C4 vs 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws) {
     constexpr int FGS = DS_FGS, NH = DS_NH;
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     static_assert(GCAP % 512 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");

@@ -457,7 +457,10 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 // num_records 0 and its loads return zeros without touching memory).
 // FGS: chunks per work item (group).
 template <int RING, int FGS>
-__global__ __launch_bounds__(256) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws) {
+#ifndef FLC_TK_WPE
+#define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     // staging per (buffer, wave): GCAP + 64 indices then GCAP + 64 values (one ds_write2st64_b32
     // per entry; the 64 spare slots take a wave-instruction starting at GCAP, i.e. an overflow)
