@@ -457,6 +457,9 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 // num_records 0 and its loads return zeros without touching memory).
 // FGS: chunks per work item (group).
 template <int RING, int FGS>
+#ifndef FLC_TK_RING
+#define FLC_TK_RING 16               // loads in flight per wave (ring registers: 4 x RING VGPRs)
+#endif
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
@@ -1767,7 +1770,7 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream
         const char* e = tuning_env("FLC_TK_RB");          // tuning runs only
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
-    hipLaunchKernelGGL((k_topk_filter_fast<16, FGS>), dim3(gw), dim3(256), 0, st, rows, n, std::min(rb, std::max<int64_t>(n, 1)), d, ws);
+    hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, std::min(rb, std::max<int64_t>(n, 1)), d, ws);
 }
 
 static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
