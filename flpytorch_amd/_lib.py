@@ -25,9 +25,9 @@ FLC_PATH_AUTO, FLC_PATH_SPARSE, FLC_PATH_DENSE = 0, 1, 2
 def FLC_ROW_GROUPS(g):
     return (int(g) & 0xFF) << 8
 
-# every symbol include/flcodec.h declares (tests/test_abi.py checks the .so exports all of them)
+# every symbol include/flcodec.h declares (tests/test_host.py checks the .so exports all of them)
 EXPORTS = [
-    "flc_version", "flc_last_error_string",
+    "flc_version", "flc_build_id", "flc_last_error_string",
     "flc_reduce_rows", "flc_reduce_matrix",
     "flc_encode_workspace_size", "flc_encode",
     "flc_encode_reduce_workspace_size", "flc_encode_reduce",
@@ -95,6 +95,7 @@ def load():
         P = ctypes.POINTER
         lib.flc_version.restype = i32
         lib.flc_last_error_string.restype = ctypes.c_char_p
+        lib.flc_build_id.restype = ctypes.c_char_p
         lib.flc_reduce_rows.argtypes = [vp, i64, i64, vp, vp, f32, i32, vp, vp]
         lib.flc_reduce_matrix.argtypes = [vp, i64, i64, i64, vp, vp, f32, i32, vp, vp]
         lib.flc_encode_workspace_size.argtypes = [P(FlcCodecParams), i64]
@@ -138,7 +139,7 @@ def load():
         lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
         lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
         for name in EXPORTS:
-            if name not in ("flc_version", "flc_last_error_string", "flc_device_uniform",
+            if name not in ("flc_version", "flc_build_id", "flc_last_error_string", "flc_device_uniform",
                             "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
                             "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",
                             "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size",
@@ -146,6 +147,41 @@ def load():
                 getattr(lib, name).restype = i32
         _lib = lib
         return lib
+
+
+def source_hash(root=None):
+    """The digest flc_build_id() reports for a library built from the tree at ``root`` (default:
+    this package's tree): sha256 over csrc/*.hip, *.hpp, *.cpp in name order, csrc/Makefile, then
+    include/flcodec.h; first 16 hex digits."""
+    import glob
+    import hashlib
+    root = root or os.path.dirname(_HERE)
+    csrc = os.path.join(root, "flpytorch_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")) +
+                   glob.glob(os.path.join(csrc, "*.cpp")))
+    files += [os.path.join(csrc, "Makefile"), os.path.join(root, "include", "flcodec.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id():
+    return load().flc_build_id().decode()
+
+
+def check_provenance():
+    """Raise unless the loaded library was built from this tree's sources (a stale or foreign
+    .so would otherwise be measured and tested under this tree's name).  A FLC_LIB_VARIANT
+    library (A/B builds) is reported, not checked."""
+    bid, want = build_id(), source_hash()
+    if os.environ.get("FLC_LIB_VARIANT"):
+        return bid
+    if bid != want:
+        raise RuntimeError(f"flpytorch_amd: {LIB_PATH} was built from sources {bid}, the tree is {want} — "
+                           "rebuild with `make -C flpytorch_amd/csrc`")
+    return bid
 
 
 def check(rc, what):

@@ -72,6 +72,8 @@ class UplinkReducer:
         semantics: the caller orders it after the producers of ``rows`` and the patterns).
         ``randk_counts``: RandK device mode, the chunk counts from ``randk_counts(n, d, client0)``."""
         if stream is not None:
+            if stream.device != self.device:
+                raise ValueError(f"stream is on {stream.device}, the reducer runs on {self.device}")
             with torch.cuda.stream(stream):
                 return self._run(rows, out, weights, client0, randk_idx, uniforms, lazy_u, pnorms_out, divisor,
                                  randk_counts)

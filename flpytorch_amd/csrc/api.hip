@@ -66,6 +66,11 @@ using namespace flc;
 
 extern "C" int flc_version(void) { return 100; }
 
+#ifndef FLC_SRC_HASH
+#define FLC_SRC_HASH "unknown"
+#endif
+extern "C" const char* flc_build_id(void) { return FLC_SRC_HASH; }
+
 extern "C" int flc_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;
@@ -285,6 +290,10 @@ extern "C" int flc_device_randk_counts(uint64_t seed, int64_t client0, int64_t n
     if (n < 1 || d < 1 || k < 1 || k > d || d >= (int64_t)0xFFFFFFFF || !d_counts) {
         set_error("flc_device_randk_counts: bad arguments");
         return FLC_ERR_ARG;
+    }
+    if (n > FLC_MAX_ROWS) {   // k_randk_counts indexes rows by blockIdx.y
+        set_error("flc_device_randk_counts: n=%lld rows, at most %d per call", (long long)n, FLC_MAX_ROWS);
+        return FLC_ERR_UNSUPPORTED;
     }
     return randk_device_counts(seed, client0, n, d, k, d_counts, d_ws, ws_bytes, (hipStream_t)stream);
 }

@@ -323,12 +323,18 @@ class Simulation:
                 client.sendPayload(msg)
             except Exception as e:                      # surfaced after the join
                 err.append(e)
-        t = threading.Thread(target=send)
+        t = threading.Thread(target=send, daemon=True)
         t.start()
         try:
             got = server.recvPayload(comp, d)
-        finally:
-            t.join()
+        except BaseException:
+            # a refused or broken message: unblock the sender (it may sit in sendall on a full
+            # socket buffer) before waiting for it
+            server.abort()
+            client.abort()
+            t.join(timeout=30)
+            raise
+        t.join()
         if err:
             raise err[0]
         return got

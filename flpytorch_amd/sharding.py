@@ -140,7 +140,9 @@ class ShardedUplink:
         for i, b in enumerate(blocks):
             b_lo, b_hi = client_block(n_clients, self.n_blocks, b)
             if b_hi == b_lo:
-                self._parts[i].zero_()
+                # an empty block's partial is the additive identity -0: adding it keeps a column
+                # that is -0 in every real block at -0, as the sequential fold does
+                self._parts[i].fill_(-0.0)
             elif callable(rows):
                 self.encode_partial(rows(b_lo, b_hi), b_lo, self._parts[i])
             else:

@@ -76,6 +76,13 @@ class PayloadSocket:
     def rawRecvString(self):
         return bytes(self.rawRecv()).decode("utf-8")
 
+    def abort(self):
+        """Shut the connection down in both directions (after a protocol error)."""
+        try:
+            self.sock.shutdown(socket.SHUT_RDWR)
+        except OSError:
+            pass
+
     # -- wire messages ---------------------------------------------------------------------------
     def sendPayload(self, payload):
         """Send one wire message (a uint8 tensor on the GPU or the host, or bytes)."""
@@ -94,6 +101,9 @@ class PayloadSocket:
         want = compressor.payloadBytes(d)
         n = self._recv_prefix()
         if n != want:
+            # the body is never read, so the stream is out of step: end the connection (the peer's
+            # pending send fails instead of blocking on a full socket buffer)
+            self.abort()
             raise ValueError(f"recvPayload: message of {n} bytes, the codec's payload is {want}")
         buf = self._recv_exact(n)
         compressor.validatePayload(buf, d)

@@ -101,6 +101,11 @@ typedef struct {
  * Library info / errors
  * -------------------------------------------------------------------------------------- */
 int flc_version(void);                    /* ABI version (major*100 + minor) */
+/* Build provenance: the first 16 hex digits of sha256 over the library's sources (csrc: .hip,
+ * .hpp and .cpp files in name order, then csrc/Makefile and this header), fixed at build time; "+x" is
+ * appended when extra compile flags (XFLAGS) were given.  flpytorch_amd._lib.source_hash()
+ * computes the same digest from a tree, so a stale .so is detected before it is measured. */
+const char* flc_build_id(void);
 const char* flc_last_error_string(void);  /* thread-local detail of the last failure */
 
 /* ----------------------------------------------------------------------------------------

@@ -25,6 +25,13 @@ def test_library_exports_every_header_symbol():
     assert lib.flc_version() == 100
 
 
+def test_library_build_id_matches_tree():
+    """Provenance: the shipped .so reports the digest of the sources it was built from, and it is
+    this tree's (smoke() and bench.py refuse a stale library the same way)."""
+    assert _lib.build_id() == _lib.source_hash()
+    assert _lib.check_provenance() == _lib.source_hash()
+
+
 def test_library_is_gfx950():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data

@@ -78,10 +78,31 @@ def test_recv_payload_refuses_wrong_length_before_the_body():
     c.sock.sendall(b"64:")                        # the codec's message is 16 + 112 bytes
     with pytest.raises(ValueError, match="128"):
         s.recvPayload(comp)
-    good = dense_msg(Q8, 100, bytes([0x80 | 3, 10] + [0] * 98))
-    c.rawSend(good)
-    t = s.recvPayload(comp)
-    assert t.numel() == comp.payloadBytes() == 128 and bytes(t.numpy()) == good
+    # the body was never read, so the stream is out of step: the receiver ends the connection
+    with pytest.raises(RuntimeError, match="broken"):
+        s.recvPayload(comp)
+
+
+def test_refused_length_unblocks_a_large_pending_send():
+    """A wrong-length message larger than the socket buffer: the receiver refuses it from the prefix
+    and shuts the connection down, so the sender's sendall fails instead of blocking forever."""
+    import threading
+    comp = initCompressor("qsgd:10", 100)
+    c, s = transport.socket_pair()
+    big = np.zeros(64 << 20, np.uint8)
+    err = []
+
+    def send():
+        try:
+            c.rawSend(big)
+        except OSError as e:
+            err.append(e)
+    t = threading.Thread(target=send, daemon=True)
+    t.start()
+    with pytest.raises(ValueError, match="128"):
+        s.recvPayload(comp)
+    t.join(timeout=30)
+    assert not t.is_alive() and err
 
 
 def test_validate_dense_formats():
