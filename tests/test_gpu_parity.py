@@ -138,12 +138,18 @@ def test_compress_vector_golden(ag, i, where):
             comp2.testp = comp.testp
             got = comp2._encode_gpu(x.cuda(), pnorm_in=torch.tensor([pn[c]], dtype=torch.float32, device="cuda"))
             assert_bitexact(got, want)
-            # (b) own norm: within the norm's relative difference
+            # (b) own norm: within the norms' ratio, except for decisions the norm difference flips.
+            # A flip needs the uniform between the two probabilities; for std dithering (levels
+            # 1/s apart) |dp_j| = s |x_j| rel / n, so E[flips] = s rel ||x||_1 / n.  Natural
+            # dithering's output is y * sign * pnorm whatever the level (compressors.py:326): none.
             pno = torch.empty(1, device="cuda")
             own = comp2._encode_gpu(x.cuda(), pnorm_out=pno)
             rel = abs(float(pno.item()) / pn[c] - 1.0)
             ok = np.isclose(own.cpu().numpy(), want, rtol=4 * rel + 4 * 2.0 ** -24, atol=0)
-            assert np.mean(~ok) <= 0.01
+            E = 0.0
+            if m["type"] == 5 and pn[c] > 0:
+                E = comp2.s * rel * float(np.abs(X[c]).astype(np.float64).sum()) / float(pn[c])
+            assert np.sum(~ok) <= E + 5 * math.sqrt(E) + 3, (int(np.sum(~ok)), E)
             # (c) own norm == the oracle's exactly rounded norm -> bit-exact vs the oracle
             o = oc.OracleCompressor(m["spec"], m["D"])
             o.testp = comp.testp.cpu().numpy()

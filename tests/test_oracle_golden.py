@@ -279,3 +279,26 @@ def test_oracle_weighted_fold_vs_reference():
         got = oc.server_gradient(x, list(rows), m["weights"])
         want = arr[f"c{c}_{m['algorithm']}_gs"]
         assert np.array_equal(np.asarray(got, np.float32).view(np.uint32), want.view(np.uint32)), m
+
+
+@pytest.mark.parametrize("name", ["topk_c3", "topk_c3_heavy", "qsgd_c4", "qsgd_c4_heavy"])
+def test_oracle_row_size_vs_reference(name):
+    """The oracle against the reference at the config row sizes (tests/golden/rows.*, made by
+    make_golden_rows.py): TopK's index set and dense output at D = 10 M; QSGD at D = 25 M given the
+    reference's torch norm — the whole output bit-identical — and the oracle's own norm exactly
+    rounded (the reference's fp32 torch norm sits `pnorm_ulps_from_exact` ulps from it)."""
+    from tests.test_gpu_rows_ref import ARR, CASES, row, sha
+    m = CASES[name]
+    x = row(m["seed"], m["D"], m["dist"])
+    assert sha(x) == m["x_sha"]
+    o = oc.OracleCompressor(m["spec"], m["D"])
+    if m["spec"].startswith("topk"):
+        out = o.compress(x)
+        np.testing.assert_array_equal(np.flatnonzero(out), ARR[f"{name}_ind"])
+        assert sha(out) == m["out_sha"]
+        return
+    o.testp = np.random.RandomState(m["pattern_seed"]).rand(m["D"])
+    assert sha(o.testp) == m["testp_sha"]
+    pref = np.uint32(m["pnorm_bits"]).view(np.float32)
+    assert sha(o.compress(x, pnorm=pref)) == m["out_sha"]
+    assert int(np.float32(o.norm(x)).view(np.uint32)) == m["exact_norm_bits"]
