@@ -188,21 +188,21 @@ def _on_gpu(step):
     return run
 
 
-ALGORITHMS = ("dcgd", "fedavg", "diana", "ef21")
+ALGORITHMS = ("dcgd", "fedavg", "diana", "ef21", "marina")
 
 
 class Simulation:
     """One experiment: ``rounds`` communication rounds of ``algorithm`` (one of ``ALGORITHMS``)
     with the client codec ``client_compressor`` (the reference's spec grammar), starting at ``x0``.
 
-    ``init_compressor`` / ``server_gradient`` / ``diana_step`` / ``ef21_step`` default to the
-    product (flpytorch_amd.aggregation: HIP codecs, HIP fold, fused shift codec); tests may pass
-    other implementations of the same protocol."""
+    ``init_compressor`` / ``server_gradient`` / ``diana_step`` / ``ef21_step`` / ``marina_step``
+    default to the product (flpytorch_amd.aggregation: HIP codecs, HIP fold, fused shift codec);
+    tests may pass other implementations of the same protocol."""
 
     def __init__(self, algorithm, client_compressor, model, x0, num_clients, clients_per_round, rounds,
                  local_lr, global_lr, local_iters=1, runtime_seed=0, device="cuda", sampling="uniform",
                  poisson_p=None, init_compressor=None, server_gradient=None, record_iterates=False, wire=False,
-                 initialize_shifts_policy="zero", diana_step=None, ef21_step=None):
+                 initialize_shifts_policy="zero", diana_step=None, ef21_step=None, marina_step=None):
         algorithm = algorithm.lower()
         if algorithm not in ALGORITHMS:
             raise ValueError(f"harness drives {', '.join(ALGORITHMS)}, not {algorithm!r}")  # algorithms.py:1954 style
@@ -234,10 +234,13 @@ class Simulation:
         self.init_compressor = init_compressor or ag.initCompressor
         self.diana_step = diana_step or _on_gpu(ag.dianaStep)
         self.ef21_step = ef21_step or _on_gpu(ag.ef21Step)
+        self.marina_step = marina_step or _on_gpu(ag.marinaStep)
         # DCGD / EF21 fold then apply the master (identity) compressor (algorithms.py:1748-1770,
-        # 1521-1546); FedAvg returns the fold (1810-1832); DIANA returns h + fold (1395-1421)
+        # 1521-1546); FedAvg and MARINA return the fold (1810-1832, 545-563); DIANA returns h + fold
+        # (1395-1421)
         default_fold = {"dcgd": ag.serverGradientMaster, "ef21": ag.serverGradientMaster,
-                        "fedavg": ag.serverGradientPlain, "diana": ag.serverGradientDIANA}[algorithm]
+                        "fedavg": ag.serverGradientPlain, "diana": ag.serverGradientDIANA,
+                        "marina": ag.serverGradientPlain}[algorithm]
         self.server_gradient = server_gradient or default_fold
         self.np_random = np.random.RandomState()
         self.np_random.seed(int(runtime_seed))                                   # run.py:343-345
@@ -262,15 +265,21 @@ class Simulation:
             self.H.update({"h0": h0.detach().clone(), "h": h0.detach().clone(), "alpha": 1.0 / (1.0 + w), "w": w})
         elif algorithm == "ef21":                                                # algorithms.py:1460-1468
             self.H["request_use_full_list_of_clients"] = True
+        elif algorithm == "marina":                                              # algorithms.py:486-492
+            # test_ber_rv = 0 forces a full-gradient first round
+            self.H.update({"x_prev": self.x.clone(), "test_ber_rv": 0.0})
 
     # algorithms.clientState (2015-2069) with the class parts: DCGD 1729-1732, FedAvg 1793-1794,
-    # DIANA 1360-1373, EF21 1471-1484
+    # DIANA 1360-1373, EF21 1471-1484, MARINA 495-509
     def client_state(self, client_id, rnd):
         cs = {}
-        if self.algorithm in ("dcgd", "diana", "ef21"):
+        if self.algorithm in ("dcgd", "diana", "ef21", "marina"):
             comp = self.init_compressor(self.H["client_compressor"], self.D)
             comp.generateCompressPattern(self.np_random, str(self.device), client_id, self.H)
             cs["client_compressor"] = comp
+        if self.algorithm == "marina":
+            p = 1.0 / (1.0 + comp.getW())
+            cs.update({"p": p, "ck": 1 if self.H["test_ber_rv"] <= p else 0})
         if self.algorithm == "diana":
             hi = find_recent_and_remove(self.H, client_id, "hi")
             cs["hi"] = self.H["h0"].detach().clone() if hi is None else hi
@@ -303,6 +312,16 @@ class Simulation:
             m, cs["hi"] = self.diana_step(comp, g, cs["hi"], self.H["alpha"])
             cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
             return m
+        if self.algorithm == "marina":                                           # algorithms.py:512-540
+            if cs["ck"] == 1:
+                cs["stats"]["send_scalars_to_master"] += g.numel()
+                return g
+            # the gradient at the previous iterate (its function value is not recorded), then
+            # g_prev + C(grad_cur - grad_prev) in one fused pass
+            _, g_old = self.model.value_and_gradient(self.H["x_prev"], cs["client_id"])
+            g_next = self.marina_step(comp, g, g_old, self.H["g_prev"].to(g.device))
+            cs["stats"]["send_scalars_to_master"] += comp.last_need_to_send_advance
+            return g_next
         if cs["g_prev"] is None:                                                 # EF21, algorithms.py:1494-1500
             cs["g_prev"] = g                                                     # (first step: not counted)
             return g
@@ -387,6 +406,10 @@ class Simulation:
         elif self.algorithm == "ef21":                                           # algorithms.py:1549-1554
             self.H["compressor_master"].generateCompressPattern(self.np_random, str(self.device), -1, self.H)
             self.H["request_use_full_list_of_clients"] = False
+        elif self.algorithm == "marina":                                         # algorithms.py:566-572
+            self.H["g_prev"] = gs
+            self.H["x_prev"] = self.x.clone()                                    # the iterate after the step
+            self.H["test_ber_rv"] = self.np_random.random()
         return self.H["history"][rnd]
 
     def run(self):

@@ -50,6 +50,21 @@ RUNS.update({
                            "--num-clients-per-round", "2", "-li", "2", "--rounds", "5"],
     "ef21_randk10_p2": ["--algorithm", "ef21", "--client-compressor", "randk:10%",
                         "--num-clients-per-round", "2", "--rounds", "5"],
+    # Poisson client sampling (fl_funcs.py:17-40): per round and client one uniform() draw; the
+    # plain form allows empty rounds (serverGradient -> zeros, algorithms.py:2117-2118), the
+    # no-empty form redraws the whole round until someone is sampled
+    "dcgd_randk10_poisson": ["--algorithm", "dcgd", "--client-compressor", "randk:10%",
+                             "--client-sampling-type", "poisson", "--client-sampling-poisson", "0.3",
+                             "--rounds", "8"],
+    "fedavg_poisson_no_empty": ["--algorithm", "fedavg", "--client-compressor", "ident",
+                                "--client-sampling-type", "poisson-no-empty", "--client-sampling-poisson", "0.3",
+                                "--rounds", "8"],
+    # MARINA (algorithms.py:480-573): the server's np_random.random() after every round (571)
+    # decides full gradients vs g_prev + C(grad - grad_prev) for the next round
+    "marina_randk10_li2": ["--algorithm", "marina", "--client-compressor", "randk:10%", "-li", "2",
+                           "--rounds", "8"],
+    "marina_qsgd10_p2_li2": ["--algorithm", "marina", "--client-compressor", "qsgd:10", "-li", "2",
+                             "--num-clients-per-round", "2", "--rounds", "8"],
 })
 
 
@@ -71,12 +86,14 @@ def main():
 
     # the iterate after every round's global step (the model holds it when serverGlobalStateUpdate
     # runs, model_funcs.py:605-607); x0 from the start hook (run.py prunes tensors from H at the end)
-    iterates, starts, shifts = [], [], []
+    iterates, starts, shifts, ber = [], [], [], []
     orig_sgsu = algorithms.serverGlobalStateUpdate
 
     def sgsu_wrap(clients_responses, model, *a, **k):
         iterates.append(mutils.get_params(model).detach().cpu().numpy().copy())
         Hn = orig_sgsu(clients_responses, model, *a, **k)
+        if "test_ber_rv" in Hn:
+            ber.append(Hn["test_ber_rv"])                                # MARINA's server draw
         if Hn["algorithm"] == "diana":
             shifts.append(Hn["h"].detach().cpu().numpy().copy())         # h after h += alpha m
         return Hn
@@ -98,6 +115,7 @@ def main():
         iterates.clear()
         starts.clear()
         shifts.clear()
+        ber.clear()
         result = {}
         execution_context.simulation_finish_fn = lambda H, _r=result: _r.update(H=H)
         refrun.runSimulation(mg.COMMON + extra + ["--run-id", name])
@@ -133,6 +151,9 @@ def main():
             "manual_runtime_seed": int(args.manual_runtime_seed), "samples_per_client": int(S),
             "D": int(H["D"]), "history": rounds,
             "initialize_shifts_policy": args.initialize_shifts_policy,
+            "client_sampling_type": args.client_sampling_type,
+            "client_sampling_poisson": float(args.client_sampling_poisson),
+            "test_ber_rv": [float(v) for v in ber],
         }
         print(name, [r["grad_sgd_server_l2"] for r in rounds])
     np.savez_compressed(os.path.join(HERE, "harness.npz"), **arrays)

@@ -35,7 +35,8 @@ def test_harness_reproduces_reference_run(ag, name, device):
     folds = []
     algo = META[name]["algorithm"]
     default_fold = {"dcgd": ag.serverGradientMaster, "ef21": ag.serverGradientMaster,
-                    "fedavg": ag.serverGradientPlain, "diana": ag.serverGradientDIANA}[algo]
+                    "fedavg": ag.serverGradientPlain, "diana": ag.serverGradientDIANA,
+                    "marina": ag.serverGradientPlain}[algo]
 
     def recording_fold(buf, clients, model, x, H):
         rows = [buf.get(i)["model"].detach().cpu().numpy().copy() for i in range(clients)]
@@ -61,11 +62,12 @@ def test_harness_reproduces_reference_run(ag, name, device):
         assert np.array_equal(gs.view(np.uint32), want.view(np.uint32))
 
 
-@pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] in ("diana", "ef21")])
+@pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] in ("diana", "ef21", "marina")])
 def test_harness_shift_steps_run_fused_codec(ag, name):
-    """DIANA / EF21 client steps go through the fused shift codec (Compressor.compressShift ->
-    flc_encode_shift), and each step is bit-identical to the reference's torch expression on the
-    same inputs (algorithms.py:1386-1391, 1508-1513) evaluated with the product's compressVector."""
+    """DIANA / EF21 / MARINA client steps go through the fused shift codec (Compressor.compressShift
+    -> flc_encode_shift), and each step is bit-identical to the reference's torch expression on the
+    same inputs (algorithms.py:1386-1391, 1508-1513, 536-537) evaluated with the product's
+    compressVector."""
     calls = []
     orig = ag.Compressor.compressShift
 
@@ -87,7 +89,7 @@ def test_harness_shift_steps_run_fused_codec(ag, name):
             assert torch.equal(msg.view(torch.int32), c.view(torch.int32))
             assert torch.equal(hout.view(torch.int32), want_h.view(torch.int32))
         else:
-            want = kw["base"] + c * kw["scale"]
+            want = kw["base"] + c * kw.get("scale", 1.0)        # MARINA: g_prev + C(.) (scale 1)
             assert torch.equal(msg.view(torch.int32), want.view(torch.int32))
 
 

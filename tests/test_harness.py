@@ -68,10 +68,15 @@ def oracle_ef21_step(comp, g, g_prev):
     return g_prev + comp.compressVector(g - g_prev) * mult               # algorithms.py:1508-1513
 
 
+def oracle_marina_step(comp, g, g_old, g_prev):
+    return g_prev + comp.compressVector(g - g_old)                       # algorithms.py:536-537
+
+
 def oracle_simulation(name, **kw):
     fold = oracle_server_gradient_diana if META[name]["algorithm"] == "diana" else oracle_server_gradient
     return simulation(name, "cpu", init_compressor=OracleCompressorDouble, server_gradient=fold,
-                      diana_step=oracle_diana_step, ef21_step=oracle_ef21_step, **kw)
+                      diana_step=oracle_diana_step, ef21_step=oracle_ef21_step, marina_step=oracle_marina_step,
+                      **kw)
 
 
 def run_collecting_shift(sim):
@@ -134,7 +139,7 @@ def test_rejects_other_algorithms():
     from flpytorch_amd import harness
     m = harness.DenseModel(DATA["data_A"], DATA["data_B"], 16)
     with pytest.raises(ValueError):
-        harness.Simulation("marina", "ident", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu")
+        harness.Simulation("scaffold", "ident", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu")
     with pytest.raises(ValueError):
         harness.Simulation("diana", "randk:10%", m, np.zeros(m.D, np.float32), 4, 4, 1, 0.1, 1.0, device="cpu",
                            wire=True)
@@ -164,3 +169,28 @@ def test_ef21_first_round_samples_every_client():
     assert sim.H["request_use_full_list_of_clients"] is False
     sim.run_round(1)
     assert list(sim.H["history"][1]["client_states"]) == [int(c) for c in sim.sampled[1]]
+
+
+@pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] == "marina"])
+def test_marina_server_draws_follow_the_stream(name):
+    """MARINA's serverGlobalStateUpdate draws np_random.random() after every round (algorithms.py:571):
+    the harness's draws equal the reference run's, and each round's clients took the full-gradient
+    branch exactly when the previous draw was <= p = 1 / (1 + w)."""
+    sim = oracle_simulation(name)
+    draws = []
+    for r in range(sim.rounds):
+        prev = sim.H["test_ber_rv"]
+        sim.run_round(r)
+        draws.append(sim.H["test_ber_rv"])
+        for st in sim.H["history"][r]["client_states"].values():
+            cs = st["client_state"]
+            assert cs["ck"] == (1 if prev <= cs["p"] else 0)
+    assert draws == META[name]["test_ber_rv"]
+
+
+def test_poisson_runs_include_an_empty_round():
+    """The Poisson fixture exercises fl_funcs.py:17-29's empty sample: zero clients, zero gradient."""
+    m = META["dcgd_randk10_poisson"]
+    empty = [r for r, h in enumerate(m["history"]) if not h["clients"]]
+    assert empty and all(m["history"][r]["grad_sgd_server_l2"] == 0.0 for r in empty)
+    assert all(h["clients"] for h in META["fedavg_poisson_no_empty"]["history"])
