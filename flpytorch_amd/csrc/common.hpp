@@ -220,7 +220,28 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
 // quarter hash per element (the sparse QSGD candidate filter, dither_sparse.hip).
 __host__ __device__ inline uint32_t colbase(uint32_t j) { return j * 0x85EBCA77u; }
 __host__ __device__ inline uint32_t rowkey(uint64_t ckey) { return (uint32_t)(ckey >> 32) ^ (uint32_t)ckey; }
-__host__ __device__ inline uint32_t grouphash(uint32_t g, uint32_t rk) { return fmix32(g * 0x9E3779B1u + rk); }
+#ifndef FLC_GHASH
+#define FLC_GHASH 0
+#endif
+__host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+// A/B candidates for the group hash (FLC_GHASH, tuning builds): 1 = two rounds of a 24-bit
+// multiply (full rate v_mul_u32_u24) with the ignored top byte folded back in; 2 = 32x32->64
+// multiply folded (lo ^ hi)
+__host__ __device__ inline uint32_t gmix(uint32_t v) {
+#if FLC_GHASH == 1
+    uint32_t h = v ^ (v >> 16);
+    h = mul24(h, 0xB5297Au | 1u) ^ (h >> 24);
+    h ^= h >> 16;
+    h = mul24(h, 0x68E31Du) ^ (h >> 24);
+    return h ^ (h >> 16);
+#elif FLC_GHASH == 2
+    const uint64_t p = (uint64_t)v * (uint64_t)(v ^ 0x2D358DCCu);
+    return (uint32_t)p ^ (uint32_t)(p >> 32);
+#else
+    return fmix32(v);
+#endif
+}
+__host__ __device__ inline uint32_t grouphash(uint32_t g, uint32_t rk) { return gmix(g * 0x9E3779B1u + rk); }
 __host__ __device__ inline uint32_t draw_join(uint32_t hg, uint32_t q, uint32_t lo) {
     return ((hg >> (8u * q)) << 24) | (lo >> 8);
 }

@@ -79,10 +79,11 @@ constexpr int64_t DS_RB = 16;
 // One entry of the fold's lists (u16): half-chunk-local index (11 bits) | sign << 11 | level << 12;
 // its contribution is copysign(levels[level], sign) * norm — C(x) exactly as the encode forms it.
 struct DsWs {
-    uint2* tabs;          // [Hp][N] (offset, count) of row's sure entries in half chunk h: the
-                          // list of (h, row) is ent16[row][offset .. offset + count + cntr)
+    uint2* tabs;          // [Hp][N] (unused, count) of row's sure entries in half chunk h: the
+                          // list of (h, row) is ent16[h][row][0 .. count + cntr)
     uint32_t* cntr;       // [Hp][N] resolved entries appended after them (k_ds_resolve)
-    uint16_t* ent16;      // [N][cap] entries; item region = NH halves x DS_HCAP
+    uint16_t* ent16;      // [Hp][N][DS_HCAP] entries, half-major: the fold of half h reads its
+                          // rows' regions as one contiguous n * 256-byte run
     uint2* enta;          // [N][cap] ambiguous candidates (item-local index | hi8 << 13, x bits)
     uint32_t* itm;        // [G][N] ambiguous candidates of the item; DS_OVF: it overflowed
     uint32_t* flags;      // [N] DS_*
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
                 const float4 x = ring[L % RING];
                 uint32_t hg;
                 if (PROBE == 4) { hg = gb + (uint32_t)(L * 64) * 0x9E3779B1u; hg ^= hg >> 15; }   // cost probe only
-                else hg = fmix32(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
+                else hg = gmix(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
 #pragma unroll
             for (int v = 0; v < NH; ++v) hc = (uint32_t)v == u ? hs[v] : hc;
             // halves past the row end land in the tab's padding rows (G * NH >= H)
-            ws.tabs[(gi * NH + u) * n + row] = make_uint2(base + u * DS_HCAP, ovf ? 0u : hc);
+            ws.tabs[(gi * NH + u) * n + row] = make_uint2(0u, ovf ? 0u : hc);
         }
         {
             // sure entries: lane l holds entries 8 (l % 16) .. + 8 of half l / 16; slots past the
@@ -404,10 +405,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
 #pragma unroll
             for (int v = 0; v < NH; ++v) hc = (uint32_t)v == u ? hs[v] : hc;
             const bool put = !ovf && k8 < hc;
-            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.ent16 + row * ws.cap + base, (short)0, GCAP * 2, 0x00020000);
+            // half u's region of this row: ent16[gi * NH + u][row], n * DS_HCAP entries apart
+            const uint32_t hstride = (uint32_t)n * (DS_HCAP * 2);               // bytes
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.ent16 + ((int64_t)gi * NH * n + row) * DS_HCAP, (short)0,
+                                                              (int)((NH - 1) * hstride + DS_HCAP * 2), 0x00020000);
             const uint4 v = reinterpret_cast<const uint4*>(s16)[lane];
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od,
-                                                   put ? lane * 16 : 0x7FFFFFF0, 0, 0);
+                                                   put ? u * hstride + k8 * 2u : 0x7FFFFFF0u, 0, 0);
         }
         {
             // ambiguous entries: two per lane per 16-B store; an odd count's last slot is stale
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(256) void k_ds_resolve(int64_t n, int64_t r0, int64
                 if (l.idx > DS_MAXLEV || pos >= (uint32_t)DS_HCAP) {
                     atomicOr(&ws.flags[rk_], DS_DENSE);
                 } else {
-                    ws.ent16[rk_ * ws.cap + (int64_t)gk * DS_GCAP + u * DS_HCAP + pos] =
+                    ws.ent16[(((int64_t)gk * NH + u) * n + rk_) * DS_HCAP + pos] =
                         (uint16_t)((loc & (HCHUNK - 1)) | ((en.y >> 31) << 11) | ((uint32_t)l.idx << 12));
                 }
             }
@@ -699,7 +703,8 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
         // the array's first 64 entries instead
         auto fetch = [&](const DsMeta& m, int q, int64_t row, int slot) {
             const uint32_t off = __builtin_amdgcn_readlane(m.off, q), cnt = __builtin_amdgcn_readlane(m.cnt, q);
-            const uint16_t* p = cnt ? ws.ent16 + row * ws.cap + off : ws.ent16;
+            const uint16_t* p = cnt ? ws.ent16 + (h * n + row) * DS_HCAP : ws.ent16;
+            (void)off;
             const uint32_t v = p[lane];
             ra[slot] = (uint32_t)lane < cnt ? v : NONE;
         };
@@ -768,9 +773,9 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
                                 const float e = value(a, pn);
                                 add(a & (HCHUNK - 1), W ? wi * e : e);
                             }
-                            const uint32_t cnt = __builtin_amdgcn_readlane(cur.cnt, q), off = __builtin_amdgcn_readlane(cur.off, q);
+                            const uint32_t cnt = __builtin_amdgcn_readlane(cur.cnt, q);
                             for (uint32_t e = 64u + lane; e < cnt; e += 64) {
-                                const uint32_t en = ws.ent16[row * ws.cap + off + e];
+                                const uint32_t en = ws.ent16[(h * n + row) * DS_HCAP + e];
                                 const float ev = value(en, pn);
                                 add(en & (HCHUNK - 1), W ? wi * ev : ev);
                             }
