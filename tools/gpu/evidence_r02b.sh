@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 (second half) evidence pass on one GPU box: tests, smoke, PMC traffic, rocprof stats,
-# bench lines.  Output under gpurun_out/ev3; copy what is judged into profiles/r02b.
+# bench lines.  Output under gpurun_out/ev3; copy what is judged into profiles/archive/r02b.
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 out=gpurun_out/ev3
