@@ -51,7 +51,7 @@ WORKLOADS = {
                others=["k_randk_counts", "k_chunk_accum"]),
     # sparse QSGD path (dither_sparse.hip): one read of every row in k_ds_filter
     "c4": dict(spec="qsgd:127", n=512, d=25_000_000, kernel="k_ds_filter", config=3, n_total=4096,
-               others=["k_ds_sample", "k_ds_accum"]),
+               others=["k_ds_sample", "k_ds_resolve", "k_ds_accum"]),
     # C5: mixed per-client codec (client i -> specs[i % 3]); a pool of resident distinct rows is
     # replayed through the clients' row pointers (819 GB of distinct rows per GPU would not fit)
     "c5": dict(spec="mixed", specs=["randk:1%", "topk:1%", "qsgd:127"], n=2048, d=100_000_000, pool=384,
@@ -390,8 +390,16 @@ def dropin(args):
     """The drop-in path as the reference's algorithms drive it after install(): every client's
     Compressor.compressVector (generateCompressPattern on the caller's numpy stream first: compat
     mode, the reference's own draws) and then the serverGradient fold of the N dense outputs
-    (reduce_rows) — against the fused uplink (UplinkReducer) on the same rows.  Own line, not value."""
+    (reduce_rows) — against the fused uplink (UplinkReducer) on the same rows.  Own line, not value.
+
+    roofline: the bytes the protocol mandates (algorithms.py:1735-1745 -> compressors.py:218-371,
+    then 1753-1768): a compressVector reads x and writes the dense [D] output (8 D; dithering in
+    compat mode also reads the float64 uniforms, 8 D), the fold reads the N dense outputs and
+    writes gs (4 N D + 4 D).  Device time of one compressVector from HIP events around the call
+    on its stream (many calls, mean), of the fold likewise."""
+    from flpytorch_amd import _lib
     from flpytorch_amd import aggregation as ag
+    _lib.check_provenance()
     wl = dict(WORKLOADS[args.workload])
     n = args.n or 32
     d = args.d or wl["d"]
@@ -403,6 +411,9 @@ def dropin(args):
     x = torch.zeros(d, device=dev)
     comps = [ag.initCompressor(spec, d) for _ in range(n)]
     rs = np.random.RandomState(123)
+    dither = spec.startswith(("qsgd", "std_dithering", "natural", "terngrad"))
+    for i in range(n):                              # compat patterns drawn once (host numpy stream)
+        comps[i].generateCompressPattern(rs, "cuda", i, {})
 
     def per_client(patterns=True):
         outs = []
@@ -411,6 +422,34 @@ def dropin(args):
                 comps[i].generateCompressPattern(rs, "cuda", i, {})
             outs.append(comps[i].compressVector(rows[i]))
         return ag.reduce_rows(x, outs, relative=False)
+
+    def dev_time(fn, reps):
+        """mean device ms of fn() (HIP events on the current stream, which the library launches on)"""
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    # one compressVector at a time (the reference's serial round order), patterns resident
+    if dither:
+        for c in comps:                             # the uniforms on the device once (the protocol's lazy .to)
+            c.testp = c.testp.to(dev)
+    reps = max(args.steps, 20)
+    cv_ms = dev_time(lambda: comps[0].compressVector(rows[0]), reps)
+    outs = [comps[i].compressVector(rows[i]) for i in range(n)]
+    fold_ms = dev_time(lambda: ag.reduce_rows(x, outs, relative=False), max(args.steps, 5))
+    cv_bytes = 8 * d + (8 * d if dither else 0)
+    fold_bytes = 4 * n * d + 4 * d
+
+    def rate(b, ms):
+        gbs = b / (ms * 1e-3) / 1e9
+        return {"ms": round(ms, 4), "bytes": b, "GBps": round(gbs, 1), "frac": round(gbs / PEAK_GBS, 4)}
 
     red = ag.UplinkReducer(ag.initCompressor(spec, d), device=dev, seed=5)
     res = {}
@@ -425,8 +464,34 @@ def dropin(args):
             fn()
         torch.cuda.synchronize()
         res[name] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
-    print(json.dumps({"mode": "drop-in path (compressVector per client + serverGradient fold) vs fused uplink",
-                      "codec": spec, "clients": n, "D": d, "ms_per_round": res,
+    # per-kernel device time of one compressVector (flc_profile scopes)
+    kernels = ["k_topk_sample", "k_topk_filter", "k_cand_select", "k_topk_exact_rows", "k_chunk_accum",
+               "k_norm_partials", "k_ew_accum_vec", "k_ew_encode", "k_randk_scatter_dev", "k_assign_scatter"]
+    _lib.profile_enable(True)
+    for k in kernels:
+        _lib.profile_collect(k)
+    for _ in range(10):
+        comps[0].compressVector(rows[0])
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    per_kernel = {}
+    for k in kernels:
+        ms, cnt = _lib.profile_collect(k)
+        if cnt:
+            per_kernel[k] = round(ms / cnt * 1e3, 2)
+    cv = rate(cv_bytes, cv_ms)
+    print(json.dumps({"metric": "drop-in compressVector + serverGradient fold, device time; % HBM peak",
+                      "mode": "drop-in path (compressVector per client + serverGradient fold) vs fused uplink",
+                      "codec": spec, "clients": n, "D": d,
+                      "roofline": {"bound": "hbm", "kernel": "compressVector (one row)", "achieved": cv["GBps"],
+                                   "peak": PEAK_GBS, "unit": "GB/s", "frac": cv["frac"], "traffic": None,
+                                   "bytes_per_call": cv_bytes, "us_per_call": round(cv_ms * 1e3, 2),
+                                   "per_kernel_us": per_kernel,
+                                   "bytes_note": "read x + write the dense output (8 D)"
+                                                 + (" + the float64 uniforms (8 D)" if dither else "")},
+                      "fold": rate(fold_bytes, fold_ms),
+                      "round_device_ms": round(n * cv_ms + fold_ms, 4),
+                      "ms_per_round": res,
                       "note": "compat mode draws the reference's numpy stream on the host (MT19937 in C++) "
                               "and uploads it; the second line reuses the drawn patterns"}))
 
@@ -670,7 +735,7 @@ def main():
     achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
     line_floor = None
     if wl["kernel"] in ("k_randk_fold", "k_randk_gen"):
-        # sparse 4-B gathers fetch whole 128-B lines (profiles/r02/probe_gather_fetch.txt): the
+        # sparse 4-B gathers fetch whole 128-B lines (profiles/archive/r02/probe_gather_fetch.txt): the
         # gather's physical floor is the expected number of distinct lines touched, x 128 B
         nr = len(range(specs.index("randk:1%"), n, len(specs))) if mixed else n
         line_floor = nr * (d / 32.0) * (1.0 - (1.0 - k / d) ** 32) * 128 + (4 * d if wl["kernel"] == "k_randk_fold" else 0)

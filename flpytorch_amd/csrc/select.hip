@@ -39,6 +39,8 @@ constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
 constexpr int SMAX = 16384;          // sample size kept in LDS
 constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
 constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
+constexpr int CS_SH = 64;            // few rows: shards of a row's candidate list (k_cs_pass workgroups)
+constexpr int64_t CS_FEW = 16;       // rows: sharded lists + k_cs_pass up to here, else k_cand_select
 
 struct SelWs {            // carved from the caller workspace
     uint2* tab;           // [C][N] (offset, count) of each row's entries in chunk c
@@ -55,6 +57,9 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* worklist;   // [N] rows on the exact path
     uint32_t* nwork;      // [1]
     uint32_t* cursor;     // [C][N] RandK scatter cursors
+    uint32_t* cstate;     // [N][4] few-row candidate select: shift, prefix, krem, stage (k_cs_pass)
+    uint32_t* carrive;    // [N * RCS] its per-row arrival counters
+    uint32_t* shcnt;      // [N][CS_SH * RCS] few rows: the filter's reservation counters, one per shard
     int64_t cap;
 };
 
@@ -119,7 +124,7 @@ __device__ inline uint32_t key_bin(uint32_t key, int p) {
 // TopK: sample threshold (one workgroup per row)
 // ------------------------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws) {
+__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few) {
     __shared__ uint32_t keys[SMAX];
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
@@ -184,7 +189,11 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
         ws.prefix[row] = kest;
         ws.flags[row] = 0;
         ws.rowcnt[(row) * RCS] = 0;
+        if (few) { ws.cstate[row * 4 + 3] = 0; ws.carrive[row * RCS] = 0; }
     }
+    if (few && threadIdx.x < CS_SH) ws.shcnt[(row * CS_SH + threadIdx.x) * RCS] = 0;
+    if (few)                                              // the row's global histogram of k_cs_pass
+        for (int i = threadIdx.x; i < HBINS; i += NT) ws.hist[row * HBINS + i] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -310,6 +319,110 @@ __global__ __launch_bounds__(NT) void k_cand_select(int64_t n, int64_t K, SelWs 
             }
         }
         __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// The same selection for a few rows (a lone compressVector), spread over the chip: each row's
+// list is split over gridDim.x workgroups that histogram their slices (LDS) into the row's global
+// histogram (atomics); the last workgroup to arrive picks the digit (the same digits, bins and
+// results as k_cand_select) and leaves the row's state for the next launch — one launch per digit
+// instead of one latency-bound workgroup walking 1.4 K candidates twice.  Ambiguous ties at the
+// K-th key send the row to the exact path (k_topk_exact_rows: the same lowest-index rule).
+// ------------------------------------------------------------------------------------------
+constexpr int CS_NT = 256;
+__global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t last_wg;
+    const int64_t row = blockIdx.y;
+    const uint32_t B = gridDim.x, b = blockIdx.x;
+    uint32_t* cs = ws.cstate + row * 4;                                 // shift, prefix, krem, stage
+    const uint32_t stage = cs[3];
+    if (stage >= 2u) return;                                             // done: the whole grid row
+    // the row's list is CS_SH shards (the filter's reservations): workgroup b walks shard b
+    const uint32_t* shc = ws.shcnt + row * CS_SH * RCS;
+    uint32_t cnt = 0;
+    for (int k = 0; k < CS_SH; ++k) cnt += shc[k * RCS];
+    const uint32_t mycnt = shc[b * RCS];
+    const bool first = stage == 0u;
+    if (first && (ws.flags[row] != 0u || cnt < (uint32_t)K)) {          // overflowed / sample too high
+        if (b == 0 && threadIdx.x == 0) {
+            if (ws.flags[row] == 0u) ws.flags[row] = F_SHORT;
+            cs[3] = 2u;
+        }
+        return;
+    }
+    const uint32_t T = ws.thr[row];
+    uint32_t sh, prefix, krem;
+    if (first) {
+        const uint32_t span = ws.prefix[row] - T;                        // kest >= T
+        uint32_t s0 = 0;
+        while (s0 < 21 && (((uint64_t)span * 4u) >> s0) >= (uint64_t)HBINS) ++s0;
+        sh = s0; prefix = 0; krem = (uint32_t)K;
+    } else {
+        sh = cs[0]; prefix = cs[1]; krem = cs[2];
+    }
+    const uint32_t s1 = first ? sh : (sh > 11u ? sh - 11u : 0u);
+    const uint32_t mask = first ? 0xFFFFFFFFu : ((1u << (sh - s1)) - 1u);
+    for (int i = threadIdx.x; i < HBINS; i += CS_NT) h[i] = 0;
+    __syncthreads();
+    auto add = [&](float x) {
+        const uint32_t dk = mag_key(x) - T;
+        if (first) atomicAdd(&h[min(dk >> s1, (uint32_t)(HBINS - 1))], 1u);
+        else if ((dk >> sh) == prefix) atomicAdd(&h[(dk >> s1) & mask], 1u);
+    };
+    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
+    const float* vals = ws.ent_val + row * ws.cap + b * segcap;          // 16 B aligned shards
+    const float4* v4 = reinterpret_cast<const float4*>(vals);
+    const uint32_t n4 = mycnt >> 2, q1 = n4;
+    uint32_t i = threadIdx.x;
+    for (; i + 3 * CS_NT < q1; i += 4 * CS_NT) {
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = cs_ld(v4 + i + u * CS_NT);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { add(q[u].x); add(q[u].y); add(q[u].z); add(q[u].w); }
+    }
+    for (; i < q1; i += CS_NT) {
+        const float4 q = cs_ld(v4 + i);
+        add(q.x); add(q.y); add(q.z); add(q.w);
+    }
+    for (uint32_t t = n4 * 4 + threadIdx.x; t < mycnt; t += CS_NT) add(vals[t]);
+    __syncthreads();
+    uint32_t* gh = ws.hist + row * HBINS;
+    for (int t = threadIdx.x; t < HBINS; t += CS_NT)
+        if (h[t]) atomicAdd(gh + t, h[t]);
+    // publish: every wave's adds complete, then one release + the arrival (the last arriver picks)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last_wg = atomicAdd(&ws.carrive[row * RCS], 1u) == B - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last_wg) return;
+    // the row's histogram read and cleared with memory-side atomics: current on any XCD
+    for (int t = threadIdx.x; t < HBINS; t += CS_NT) h[t] = atomicExch(gh + t, 0u);
+    __syncthreads();
+    uint32_t bin, above;
+    hist_find(h, krem, bin, above, scratch);
+    if (threadIdx.x == 0) {
+        atomicExch(&ws.carrive[row * RCS], 0u);
+        const uint32_t last = h[bin];
+        const uint32_t np = first ? bin : ((prefix << (sh - s1)) | bin);
+        const uint32_t nk = krem - above;
+        if (first && bin == HBINS - 1) {                                 // K-th key in the clamp bin
+            ws.flags[row] |= F_SHORT;
+            cs[3] = 2u;
+        } else if (s1 == 0u) {
+            if (last > nk) ws.flags[row] |= F_SHORT;                     // ambiguous ties: exact path
+            else { ws.thr[row] = T + np; ws.krem[row] = nk; }
+            cs[3] = 2u;
+        } else {
+            cs[0] = s1; cs[1] = np; cs[2] = nk; cs[3] = 1u;
+        }
     }
 }
 
@@ -463,7 +576,7 @@ template <int RING, int FGS>
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws, int shards) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     // staging per (buffer, wave): GCAP + 64 indices then GCAP + 64 values (one ds_write2st64_b32
     // per entry; the 64 spare slots take a wave-instruction starting at GCAP, i.e. an overflow)
@@ -496,9 +609,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
         ring[L] = load_q(rs, lane, L);
         __builtin_amdgcn_sched_barrier(0);   // issue in ring order: the loop's static vmcnt waits assume it
     }
+    // few rows (shards > 1): item t reserves in shard t % shards of its row's list (a counter and a
+    // region of its own): one counter per row would serialise the reservation atomics of every
+    // wave on one address (~90 per microsecond), a lone 10 M row's ~1.2 K of them took longer than
+    // its loads
+    const int64_t segcap = shards > 1 ? (ws.cap / shards) & ~int64_t(3) : ws.cap;
     // previous group, reservation in flight
     bool pv = false;
-    int64_t prow = 0, pc0 = 0;
+    int64_t prow = 0, pc0 = 0, pseg = 0;
     uint64_t pcc = 0;                        // per-chunk counts, 16 bits each
     uint32_t ptot = 0, pres = 0;
     int par = 0;
@@ -507,7 +625,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
         bool fits = ptot <= GCAP;
         if (fits && ptot) {
             base = __shfl(pres, 0, WAVE);
-            fits = (int64_t)base + ptot <= ws.cap;
+            fits = (int64_t)base + ptot <= segcap;
+            base += (uint32_t)(pseg * segcap);                           // the shard's region
         }
         if (lane < FGS && pc0 + lane < C) {
             uint32_t off = 0, cc = 0;
@@ -598,8 +717,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
         }
         if (pv) finish(par ^ 1);
         uint32_t res = 0;
-        if (cnt && cnt <= GCAP && lane == 0) res = atomicAdd(&ws.rowcnt[(row) * RCS], cnt);
-        pv = true; prow = row; pc0 = cg0; pcc = ccp; ptot = cnt; pres = res;
+        const int64_t shard = shards > 1 ? it % shards : 0;
+        if (cnt && cnt <= GCAP && lane == 0)
+            res = atomicAdd(shards > 1 ? &ws.shcnt[(row * shards + shard) * RCS] : &ws.rowcnt[(row) * RCS], cnt);
+        pv = true; prow = row; pc0 = cg0; pcc = ccp; ptot = cnt; pres = res; pseg = shard;
         // the staging writes of this group and the copy-out reads of the buffer's next use are in
         // the wave's own program order; the fence keeps the compiler from moving LDS ops across
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1671,15 +1792,23 @@ __global__ __launch_bounds__(256) void k_randk_scatter_dev(const float* __restri
 // selected -0.0 stays -0.0 like torch's out[ind] = x[ind]): after a memset, the row's list
 // (entries [0, rowcnt), distinct indices) is scattered with the fold's admission rule — no per-chunk
 // tile walk for one row.
-__global__ __launch_bounds__(256) void k_assign_scatter(SelWs ws, float* __restrict__ out) {
-    const uint32_t cnt = ws.rowcnt[0], T = ws.thr[0], f = ws.flags[0];
+__global__ __launch_bounds__(256) void k_assign_scatter(SelWs ws, float* __restrict__ out, int sharded) {
+    const uint32_t T = ws.thr[0], f = ws.flags[0];
     const uint32_t mode = (f & F_EXACT) ? 2u : ((f & F_TIES) ? 1u : 0u);
     const uint32_t cut = mode == 1u ? ws.tiecut[0] : 0xFFFFFFFFu;
-    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < cnt; e += gridDim.x * 256u) {
-        const uint32_t ix = ws.ent_idx[e];
-        const float v = ws.ent_val[e];
-        const uint32_t key = mag_key(v);
-        if (mode == 2u || key > T || (key == T && ix <= cut)) out[ix] = v;
+    // the list: [0, rowcnt) (one reservation counter, or rewritten by the exact path), else the
+    // filter's CS_SH shards, block b taking shards b, b + gridDim.x, ...
+    const bool shd = sharded && mode != 2u;
+    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
+    for (int sh = shd ? (int)blockIdx.x : 0; sh < (shd ? CS_SH : 1); sh += shd ? (int)gridDim.x : 1) {
+        const uint32_t cnt = shd ? ws.shcnt[sh * RCS] : ws.rowcnt[0];
+        const int64_t o = shd ? sh * segcap : 0;
+        for (uint32_t e = (shd ? 0u : blockIdx.x * 256u) + threadIdx.x; e < cnt; e += shd ? 256u : gridDim.x * 256u) {
+            const uint32_t ix = ws.ent_idx[o + e];
+            const float v = ws.ent_val[o + e];
+            const uint32_t key = mag_key(v);
+            if (mode == 2u || key > T || (key == T && ix <= cut)) out[ix] = v;
+        }
     }
 }
 
@@ -1716,11 +1845,17 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tiecut = cv.take<uint32_t>(nn);
         s.hist = cv.take<uint32_t>((size_t)nn * HBINS);
         s.cursor = nullptr;
+        s.cstate = cv.take<uint32_t>((size_t)nn * 4);
+        s.carrive = cv.take<uint32_t>((size_t)nn * RCS);
+        s.shcnt = cv.take<uint32_t>((size_t)std::min<int64_t>(nn, CS_FEW) * CS_SH * RCS);
     } else {
         s.tieprefix = nullptr;
         s.tiecut = nullptr;
         s.hist = nullptr;
         s.cursor = cv.take<uint32_t>((size_t)std::max<int64_t>(C, RK_SB) * nn);   // RandK: [N][RK_SB] segment offsets
+        s.cstate = nullptr;
+        s.carrive = nullptr;
+        s.shcnt = nullptr;
     }
     if (bytes) *bytes = cv.bytes();
     return s;
@@ -1751,6 +1886,16 @@ static int accum_parts() {
     return p;
 }
 
+static bool assign_fold() {          // tuning runs: FLC_ASSIGN_FOLD=1 writes a lone row's output chunk by chunk
+    static const bool v = [] { const char* e = tuning_env("FLC_ASSIGN_FOLD"); return e && atoi(e) == 1; }();
+    return v;
+}
+
+static bool cs_single() {            // tuning runs: FLC_CS_SINGLE=1 keeps the one-workgroup select for few rows
+    static const bool v = [] { const char* e = tuning_env("FLC_CS_SINGLE"); return e && atoi(e) == 1; }();
+    return v;
+}
+
 static int filter_group() {
     static const int g = [] {
         const char* e = tuning_env("FLC_FILTER_GS");     // tuning runs only
@@ -1760,7 +1905,7 @@ static int filter_group() {
 }
 
 template <int FGS>
-static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream_t st) {
+static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream_t st, int shards) {
     // oversubscribed grid (measured: 16-32 K blocks beat a resident-only persistent grid by ~5 %,
     // the hardware dispatcher balances the tail)
     const int64_t waves = n * ((nchunks(d) + FGS - 1) / FGS);
@@ -1770,7 +1915,7 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream
         const char* e = tuning_env("FLC_TK_RB");          // tuning runs only
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
-    hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, std::min(rb, std::max<int64_t>(n, 1)), d, ws);
+    hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, std::min(rb, std::max<int64_t>(n, 1)), d, ws, shards);
 }
 
 static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
@@ -1902,6 +2047,8 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (ws_bytes < need) { set_error("select: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
     SelWs ws = carve_sel(wsp, codec, n, d, K, nullptr);
     const int64_t C = host_chunks(d);
+    // TopK, few rows: sharded candidate lists (k_topk_filter_fast) and the spread select (k_cs_pass)
+    const bool few = codec == FLC_TOPK && n <= CS_FEW && !cs_single() && sel_capacity(codec, d, K) >= (int64_t)CS_SH * GCAP;
     if (codec == FLC_RANDK) {
         const int64_t ldi = pat->idx_ld ? pat->idx_ld : K;
         const int64_t spc = rk_spc(C), sb = (C + spc - 1) / spc;
@@ -1926,20 +2073,26 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         if (!dense_k) {
             { ProfScope _ps("k_topk_sample", st);
             // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3)
-            hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws); }
+            hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
+                               few ? 1 : 0); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             { ProfScope _ps("k_topk_filter", st);
             // persistent grid: exactly the resident blocks (a second partial wave of blocks would
             // leave the chip half idle at the end); buffer loads need no 16 B row alignment
             // few rows: 2-chunk groups (twice the waves in flight for a lone row)
             // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
-            if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, d, ws, st);
-            else launch_filter<4>(rows, n, d, ws, st); }
+            if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, d, ws, st, few ? CS_SH : 1);
+            else launch_filter<4>(rows, n, d, ws, st, few ? CS_SH : 1); }
             FLC_CHECK_LAUNCH("k_topk_filter");
             { ProfScope _ps("k_cand_select", st);
             // few rows (a lone compressVector): one 1024-thread workgroup per row walks the list 4x wider
             // many rows: 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
-            if (n < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)n), dim3(1024), 0, st, n, K, ws);
+            // few rows (a lone compressVector): each list over up to 64 workgroups, one launch per
+            // digit (3 cover every shift; a finished row's workgroups exit at once)
+            if (few) {
+                for (int p = 0; p < 3; ++p)
+                    hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws);
+            } else if (n < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)n), dim3(1024), 0, st, n, K, ws);
             else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(n, 8192)), dim3(512), 0, st, n, K, ws); }
             FLC_CHECK_LAUNCH("k_cand_select");
         } else {
@@ -1977,10 +2130,10 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
-    if (assign && n == 1 && codec == FLC_TOPK) {
+    if (assign && n == 1 && codec == FLC_TOPK && !assign_fold()) {
         FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
         const int sb = (int)std::max<int64_t>(1, std::min<int64_t>((sel_capacity(codec, d, K) + 255) / 256, 2048));
-        hipLaunchKernelGGL(k_assign_scatter, dim3(sb), dim3(256), 0, st, ws, out);
+        hipLaunchKernelGGL(k_assign_scatter, dim3(sb), dim3(256), 0, st, ws, out, few ? 1 : 0);
         FLC_CHECK_LAUNCH("k_assign_scatter");
         return FLC_OK;
     }

@@ -9,7 +9,10 @@ device-mode parity tests do not take their expected draws from the product libra
     ckey  = mix64(seed ^ mix64(0x9E3779B97F4A7C15 * (client + 1)))      (SplitMix64 finaliser)
     rk    = (ckey >> 32) ^ (ckey & 0xFFFFFFFF)
     lo    = fmix32(j * 0x85EBCA77 + (rk ^ 0x27D4EB2F))
-    hg    = fmix32((j >> 2) * 0x9E3779B1 + rk)                          (one per 4 elements)
+    hg    = gmix((j >> 2) * 0x9E3779B1 + rk)                            (one per 4 elements)
+    gmix(v): h = v ^ v >> 16; h = mul24(h, 0xB5297B) ^ h >> 24; h ^= h >> 16;
+             h = mul24(h, 0x68E31D) ^ h >> 24; h ^ h >> 16      (mul24 = low 32 bits of the
+             product of the low 24 bits of each operand)
     u32   = (byte (j & 3) of hg) << 24 | lo >> 8,    u = u32 * 2^-32
 """
 import numpy as np
@@ -49,9 +52,26 @@ def colbase(j):
     return np.asarray(j, dtype=np.uint32) * np.uint32(0x85EBCA77)
 
 
+def _mul24(a, b):
+    return (a & np.uint32(0xFFFFFF)) * np.uint32(b)
+
+
+def gmix(v):
+    """The group hash's mixer (common.hpp gmix, FLC_GHASH 1): two rounds of xorshift + a 24-bit
+    multiply with the ignored top byte xored back in."""
+    with np.errstate(over="ignore"):
+        h = np.asarray(v, dtype=np.uint32).copy()
+        h ^= h >> np.uint32(16)
+        h = _mul24(h, 0xB5297B) ^ (h >> np.uint32(24))
+        h ^= h >> np.uint32(16)
+        h = _mul24(h, 0x68E31D) ^ (h >> np.uint32(24))
+        return h ^ (h >> np.uint32(16))
+
+
 def grouphash(g, rk):
-    g = np.asarray(g, dtype=np.uint32)
-    return fmix32(g * np.uint32(0x9E3779B1) + np.uint32(rk))
+    with np.errstate(over="ignore"):
+        g = np.asarray(g, dtype=np.uint32)
+        return gmix(g * np.uint32(0x9E3779B1) + np.uint32(rk))
 
 
 def dev_u32(seed, client, j):

@@ -50,6 +50,15 @@ def test_harness_reproduces_reference_run(ag, name, device):
         sim.run_round(r)
         if algo == "diana":
             hs.append(sim.H["h"].detach().cpu().numpy().copy())
+    if algo == "marina":
+        # MARINA compresses the difference of two nearby gradients and carries g_prev across
+        # rounds: the model side's fp32 differences between hosts (torch's CPU / GPU kernels on
+        # the box vs the container that captured the run) flip quantisation decisions and the
+        # trajectory drifts by ~1e-3 over 8 rounds.  Bit-parity of the product is pinned against
+        # the oracle on the same box instead (test_harness_marina_matches_oracle_same_box); the
+        # oracle equals the reference exactly in the capturing container (tests/test_harness.py).
+        check_history(name, sim.H, rel=5e-3)
+        return
     check_history(name, sim.H, rel=1e-6)
     if algo == "diana":
         check_server_shift(name, hs)
@@ -60,6 +69,34 @@ def test_harness_reproduces_reference_run(ag, name, device):
     for x, rows, gs in folds:
         want = oc.server_gradient(x, rows)
         assert np.array_equal(gs.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("device", ["cpu", "cuda"])
+@pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] == "marina"])
+def test_harness_marina_matches_oracle_same_box(ag, name, device):
+    """MARINA on the product path (HIP codecs in the fused shift step, HIP fold) against the same
+    round loop driven by the oracle's codec, step and fold, with the model side on the same device
+    of the same box: every round's history scalars and iterate identical (exact float equality)."""
+    from tests.test_harness import OracleCompressorDouble, oracle_marina_step
+
+    def oracle_fold(buf, clients, model, x, H):
+        rows = [buf.get(i)["model"].detach().cpu().numpy() for i in range(clients)]
+        return torch.from_numpy(oc.server_gradient(x.detach().cpu().numpy(), rows)).to(x.device)
+
+    def oracle_step(comp, g, g_old, g_prev):
+        return oracle_marina_step(comp, g.cpu(), g_old.cpu(), g_prev.cpu()).to(g.device)
+
+    ref = simulation(name, device, init_compressor=OracleCompressorDouble, server_gradient=oracle_fold,
+                     marina_step=oracle_step, record_iterates=True)
+    sim = simulation(name, device, record_iterates=True)
+    for r in range(sim.rounds):
+        ref.run_round(r)
+        sim.run_round(r)
+        a, b = ref.H["history"][r], sim.H["history"][r]
+        for k in ("grad_sgd_server_l2", "x_before_round", "approximate_f_avg_value"):
+            assert a[k] == b[k], (name, device, r, k, a[k], b[k])
+        assert ref.H["test_ber_rv"] == sim.H["test_ber_rv"]
+        assert torch.equal(ref.iterates[r], sim.iterates[r])
 
 
 @pytest.mark.parametrize("name", [n for n in RUN_NAMES if META[n]["algorithm"] in ("diana", "ef21", "marina")])

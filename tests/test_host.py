@@ -206,6 +206,37 @@ def test_device_rng_oracle_restatement():
     assert abs(top.mean() - 127.5) < 2.0 and np.unique(top).size == 256
 
 
+@pytest.mark.parametrize("rk", [0x12345678, 0xDEADBEEF, 7])
+def test_device_rng_group_hash_statistics(rk):
+    """The group hash that supplies the draws' top bytes (common.hpp gmix over a keyed Weyl
+    sequence): over 2^20 consecutive groups, no bit is biased, no pair of bits is correlated within
+    a word or between words 1, 2, 64 or 1024 groups apart, and the 4 bytes of a group (4 elements'
+    top bytes) and neighbouring groups' bytes are jointly uniform — each statistic within what
+    independent uniform bits give (|z| < 5.5 over the ~5000 pairs, chi^2 / dof < 1.35)."""
+    import math
+    from oracle import devrng
+    n = 1 << 20
+    g = np.arange(n, dtype=np.uint32)
+    h = devrng.grouphash(g, np.uint32(rk))
+    bits = ((h[:, None] >> np.arange(32, dtype=np.uint32)) & np.uint32(1)).astype(np.float32) * 2 - 1
+    assert np.abs(bits.mean(0)).max() * math.sqrt(n) < 5.5
+    for lag in (0, 1, 2, 64, 1024):
+        a, b = (bits, bits) if lag == 0 else (bits[:-lag], bits[lag:])
+        c = (a.T @ b) / len(a)
+        if lag == 0:
+            np.fill_diagonal(c, 0)
+        assert np.abs(c).max() * math.sqrt(len(a)) < 5.5, lag
+    by = [((h >> np.uint32(8 * q)) & np.uint32(0xFF)).astype(np.int64) for q in range(4)]
+
+    def chi2(cells, bins):
+        cnt = np.bincount(cells, minlength=bins)
+        e = len(cells) / bins
+        return ((cnt - e) ** 2 / e).sum() / (bins - 1)
+    assert max(chi2(b, 256) for b in by) < 1.35
+    assert chi2((by[0] >> 6) * 64 + (by[1] >> 6) * 16 + (by[2] >> 6) * 4 + (by[3] >> 6), 256) < 1.35
+    assert chi2((by[3][:-1] >> 4) * 16 + (by[0][1:] >> 4), 256) < 1.35
+
+
 def test_c_client_of_the_abi(tmp_path):
     """include/flcodec.h compiles as C99 (-pedantic, no warnings) and a C program linked against
     libflcodec.so gets the same host-side answers as the Python binding (tests/c/abi_host.c)."""
