@@ -609,9 +609,10 @@ def main():
     compat_kw, compat_bytes, compat_note = {}, 0, None
     if args.compat and spec.startswith("randk"):
         wl["kernel"], wl["others"] = "k_randk_coarse", ["k_randk_fine", "k_chunk_accum"]
-    if args.compat and not spec.startswith("randk"):
-        # float64 uniforms go through the dense two-pass dithering path (norm pass, then the encode
-        # pass reading row + uniforms): the encode pass is the dominant kernel
+    if args.compat and not spec.startswith("randk") and wl["kernel"] != "k_ds_filter":
+        # float64 uniforms of the dense two-pass codecs (norm pass, then the encode pass reading row
+        # + uniforms): the encode pass is the dominant kernel.  QSGD (k_ds_filter) reads the
+        # uniforms beside the rows in its single pass.
         wl["kernel"], wl["others"] = "k_ew_accum_vec", ["k_norm_partials"]
     if args.compat:
         # compat mode: the reference's numpy-stream patterns, drawn on the host (the

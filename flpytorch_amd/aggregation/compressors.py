@@ -137,7 +137,7 @@ class Compressor:
         self.resetStats()
         self.device_rng = None   # (seed, client) -> device counter-based patterns (opt-in)
         # execution hints (flc_codec_params.flags); results are identical for every setting:
-        #   dither_path  None | "sparse" | "dense"  (QSGD p=2, device-RNG fused uplink)
+        #   dither_path  None | "sparse" | "dense"  (QSGD p=2 fused uplink, device-RNG or compat draws)
         #   row_groups   None | g                   (folds pipelined under the next group's pass)
         self.dither_path = None
         self.row_groups = None

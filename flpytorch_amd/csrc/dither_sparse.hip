@@ -47,6 +47,7 @@
 // intervals (y >= l1) have |x| qc >= 256.
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "chunks.hpp"
@@ -75,6 +76,7 @@ constexpr int DS_AP = FLC_DS_AP;           // rows of entry lists in flight in t
 // (and 1, row-major, 1-2 % slower on the same box); a block never reads one row twice, so rows
 // that alias (C5's replayed pool) are still read from HBM once per client
 constexpr int64_t DS_RB = 16;
+constexpr int DS_RINGC = 4;                // compat filter ring (x + u: 24 B per lane per step)
 
 // One entry of the fold's lists (u16): half-chunk-local index (11 bits) | sign << 11 | level << 12;
 // its contribution is copysign(levels[level], sign) * norm — C(x) exactly as the encode forms it.
@@ -201,19 +203,52 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
 // ------------------------------------------------------------------------------------------
 // PROBE (tuning build only, FLC_DS_PROBE; outputs NOT valid): 1 fp32 norm; 2 no candidate staging;
 // 3 loads + norm only; 4 the draw's group hash without its multiplies
-template <int RING, int GCAP, int PROBE = 0>
+//
+// COMPAT: the draws are the caller's float64 uniforms u (the reference's numpy stream, [n][uld]),
+// read in the same single pass (12 B per element).  A lane then holds elements {2l, 2l+1, 128 + 2l,
+// 128 + 2l + 1} of each 256-element step (one 512-B x load and one 1-KB u load per pair, both
+// contiguous); the candidate test takes RN(u) * 256 for the top byte, and each staged candidate
+// carries RD(u) (LDS) for its classification — the same bounds with h / 2^32 replaced by u, whose
+// float brackets [RD(u), next float up] are tighter than the 24-bit h's.
+struct CSlot {
+    float2 xa, xb;       // elements 2l, 2l+1 | 128 + 2l, 128 + 2l + 1 of the step
+    double2 ua, ub;      // their uniforms
+};
+__device__ inline CSlot load_c(__amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t ru, int lane, int L) {
+    CSlot s;
+    const auto a = __builtin_amdgcn_raw_buffer_load_b64(rx, lane * 8, L * 1024, FLC_LOADPOL);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b64(rx, lane * 8 + 512, L * 1024, FLC_LOADPOL);
+    const auto p = __builtin_amdgcn_raw_buffer_load_b128(ru, lane * 16, L * 2048, FLC_LOADPOL);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(ru, lane * 16 + 1024, L * 2048, FLC_LOADPOL);
+    s.xa = make_float2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    s.xb = make_float2(__uint_as_float(b[0]), __uint_as_float(b[1]));
+    s.ua = make_double2(__hiloint2double((int)p[1], (int)p[0]), __hiloint2double((int)p[3], (int)p[2]));
+    s.ub = make_double2(__hiloint2double((int)q[1], (int)q[0]), __hiloint2double((int)q[3], (int)q[2]));
+    return s;
+}
+// descriptor of chunk c's uniforms (range-checked like chunk_rsrc: 0 past the row end)
+__device__ inline __amdgpu_buffer_rsrc_t chunk_ursrc(const double* u, int64_t j0, int64_t d) {
+    const int64_t len = max((int64_t)0, min((int64_t)CHUNK, d - j0));
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(u + j0), (short)0, (int)(len * 8), 0x00020000);
+}
 #ifndef FLC_DS_WPE
 #define FLC_DS_WPE 6                 // 6 waves per SIMD (80 VGPRs): measured 9.19 -> 9.10 ms at C4 vs 5
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws) {
+#ifndef FLC_DS_WPEC
+#define FLC_DS_WPEC 5                // compat: 5 (LDS: 32 KB of staging per block)
+#endif
+template <int RING, int GCAP, int PROBE = 0, bool COMPAT = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FLC_DS_WPEC : FLC_DS_WPE))) void k_ds_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws, UniformSrc us) {
     constexpr int FGS = DS_FGS, NH = DS_NH;
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     static_assert(GCAP % 512 == 0 && (GCAP & (GCAP - 1)) == 0, "copy-out in whole 16-B wave slots; wrap mask");
+    static_assert(!COMPAT || PROBE == 0, "probes: device-RNG filter only");
     constexpr int DS_ITEM_STORES = 4 + GCAP / 128;   // partial, itm, tab, sure and ambiguous copy-outs
     // (entry word, x bits); 64 slots past GCAP take the writes of a wave-instruction that starts
     // at GCAP (its item has overflowed)
     __shared__ uint2 stage[4][GCAP + 64];
     __shared__ __attribute__((aligned(16))) uint16_t stage16[4][GCAP];
+    __shared__ float stagef[4][COMPAT ? GCAP + 64 : 1];     // compat: RD(u) of the staged
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t G = ws.G;
@@ -224,9 +259,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
     const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
     uint2* sg = stage[wv];
     uint16_t* s16 = stage16[wv];
+    float* sgf = stagef[wv];
     // LDS byte address of the wave's staging buffer (wave-uniform)
     const uint32_t sla = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint2*)sg);
-    float4 ring[RING];
+    typedef typename std::conditional<COMPAT, CSlot, float4>::type Slot;
+    Slot ring[RING];
     // item order: blocks of rb rows (the last one shorter), and inside a block (gi, row) with the
     // row fastest: the waves in flight at any time read the same item of the block's rows, spread
     // over rb rows rather than one row's neighbouring items, and each row is read once per launch
@@ -241,9 +278,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
     item_at(it, row, gi0);
     int64_t c = gi0 * FGS;
     auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
+    auto urow = [&](int64_t r) { return us.u + r * us.uld; };
+    auto ru = rs;
+    if constexpr (COMPAT) ru = chunk_ursrc(urow(row), c * CHUNK, d);
 #pragma unroll
     for (int L = 0; L < RING - 1; ++L) {
-        ring[L] = load_q(rs, lane, L);
+        if constexpr (COMPAT) ring[L] = load_c(rs, ru, lane, L);
+        else ring[L] = load_q(rs, lane, L);
         __builtin_amdgcn_sched_barrier(0);
     }
     {
@@ -265,70 +306,116 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
 #pragma unroll
         for (int sub = 0; sub < FGS; ++sub, ++c) {
             const int64_t j0 = c * CHUNK;
-            __amdgpu_buffer_rsrc_t rsn;
+            __amdgpu_buffer_rsrc_t rsn, run = ru;
             if (sub + 1 < FGS) {
                 rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
+                if constexpr (COMPAT) run = chunk_ursrc(urow(row), j0 + CHUNK, d);
             } else if (nit < items) {
                 int64_t ngi;
                 item_at(nit, nrow, ngi);
                 nc = ngi * FGS;
                 rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
+                if constexpr (COMPAT) run = chunk_ursrc(urow(nrow), nc * CHUNK, d);
             } else {
-                rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
-            }
-            // item-local index of (L, q): 4096 sub + 4 lane + 256 L + q (opaque: keeps the 64
-            // constants out of VGPRs); the draw's top byte is recomputed for the staged only
-            uint32_t jb = (uint32_t)lane * 4u + (uint32_t)sub * CHUNK;
-            asm volatile("" : "+v"(jb));
-            const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;   // hash input of L = 0
-#pragma unroll
-            for (int L = 0; L < 16; ++L) {
-                const int P = L + RING - 1;
-                ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
-                const float4 x = ring[L % RING];
-                uint32_t hg;
-                if (PROBE == 4) { hg = gb + (uint32_t)(L * 64) * 0x9E3779B1u; hg ^= hg >> 15; }   // cost probe only
-                else hg = gmix(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
-                const float vq[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (PROBE == 1) a2 = (double)fmaf(vq[q], vq[q], (float)a2);
-                    else a2 = fma((double)vq[q], (double)vq[q], a2);
-                    if (PROBE == 3) continue;
-                    const float hi = (float)((hg >> (8 * q)) & 0xFFu);
-                    // no range test: past the row end the loads return 0, and a zero candidate
-                    // is dropped; NaN from 0 * inf (qc = inf) is not a candidate
-                    const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
-                    const uint64_t m = __ballot(f);
-                    // exec-masked store (a branch-free store of every element to a per-lane spill
-                    // slot measured 9.2 -> 11.9 ms: the staging is LDS-issue sensitive)
-                    if (PROBE != 2 && f) {
-#if FLC_DS_W2
-                        // slot = min(cnt, GCAP) + candidates in lower lanes (< GCAP + 64): exact
-                        // while the item fits; past GCAP the item overflows (its row is folded
-                        // dense) and the writes land in the spare slots.  The scalar part is folded
-                        // into the wave's LDS address in SALU (sla), the lane part is one mbcnt
-                        // pair; index and x go out as one ds_write2_b32 (no register pair to
-                        // assemble for a 64-bit store).
-                        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        uint32_t sb = sla + min(cnt, (uint32_t)GCAP) * 8u;
-                        asm volatile("" : "+s"(sb));             // stays a scalar term: one v_lshl_add
-                        const uint32_t la = sb + pre * 8u;
-                        asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(jb + (uint32_t)(L * 256 + q)),
-                                     "v"(__float_as_uint(vq[q])) : "memory");
-#else
-                        const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
-                        sg[pos] = make_uint2(jb + (uint32_t)(L * 256 + q), __float_as_uint(vq[q]));
-#endif
-                    }
-                    cnt += (uint32_t)__popcll(m);
+                    rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
+                    if constexpr (COMPAT) run = chunk_ursrc(urow(row), 0, 0);
                 }
-                // keep the norm's fma chain here: left alone, the compiler sinks all 128 of an
-                // item's fmas to its end and holds the 128 x values live (218 VGPRs)
-                asm volatile("" : "+v"(a2));
+                if constexpr (COMPAT) {
+                    // item-local index of (L, q): 4096 sub + 2 lane + 256 L + {0, 1, 128, 129}[q]
+                    uint32_t jb = (uint32_t)lane * 2u + (uint32_t)sub * CHUNK;
+                    asm volatile("" : "+v"(jb));
+#pragma unroll
+                    for (int L = 0; L < 16; ++L) {
+                        const int P = L + RING - 1;
+                        ring[P % RING] = P < 16 ? load_c(rs, ru, lane, P) : load_c(rsn, run, lane, P - 16);
+                        const CSlot sl = ring[L % RING];
+                        const float vq[4] = {sl.xa.x, sl.xa.y, sl.xb.x, sl.xb.y};
+                        const double uq[4] = {sl.ua.x, sl.ua.y, sl.ub.x, sl.ub.y};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            a2 = fma((double)vq[q], (double)vq[q], a2);
+                            const float hf = (float)uq[q];                 // RN(u): |hf - u| <= 2^-25
+                            const bool f = fmaf(fabsf(vq[q]), qc, hf * 256.f) > DS_QT;
+                            const uint64_t m = __ballot(f);
+                            if (f) {
+                                const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                const uint32_t slot = min(cnt, (uint32_t)GCAP) + pre;
+                                sg[slot] = make_uint2(jb + (uint32_t)(L * 256 + (q & 1) + (q >> 1) * 128), __float_as_uint(vq[q]));
+                                // RD(u) (u in [0, 1): hf > u implies hf > 0)
+                                sgf[slot] = (double)hf > uq[q] ? __uint_as_float(__float_as_uint(hf) - 1u) : hf;
+                            }
+                            cnt += (uint32_t)__popcll(m);
+                        }
+                        asm volatile("" : "+v"(a2));
+                    }
+                } else {
+                // item-local index of (L, q): 4096 sub + 4 lane + 256 L + q (opaque: keeps the 64
+                // constants out of VGPRs); the draw's top byte is recomputed for the staged only
+                uint32_t jb = (uint32_t)lane * 4u + (uint32_t)sub * CHUNK;
+                asm volatile("" : "+v"(jb));
+                const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;   // hash input of L = 0
+#pragma unroll
+                for (int L = 0; L < 16; ++L) {
+                    const int P = L + RING - 1;
+                    ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
+                    const float4 x = ring[L % RING];
+                    uint32_t hg;
+                    if (PROBE == 4) { hg = gb + (uint32_t)(L * 64) * 0x9E3779B1u; hg ^= hg >> 15; }   // cost probe only
+                    else hg = gmix(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
+                    const float vq[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (PROBE == 1) a2 = (double)fmaf(vq[q], vq[q], (float)a2);
+                        else a2 = fma((double)vq[q], (double)vq[q], a2);
+                        if (PROBE == 3) continue;
+                        const float hi = (float)((hg >> (8 * q)) & 0xFFu);
+                        // no range test: past the row end the loads return 0, and a zero candidate
+                        // is dropped; NaN from 0 * inf (qc = inf) is not a candidate
+                        const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
+                        const uint64_t m = __ballot(f);
+                        // exec-masked store (a branch-free store of every element to a per-lane spill
+                        // slot measured 9.2 -> 11.9 ms: the staging is LDS-issue sensitive)
+                        if (PROBE == 5) {
+                            // A/B: the staging store without a branch — exec narrowed to the
+                            // candidates for the one ds_write2 (the loop runs with every lane active)
+                            const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            uint32_t sb = sla + min(cnt, (uint32_t)GCAP) * 8u;
+                            asm volatile("" : "+s"(sb));
+                            const uint32_t la = sb + pre * 8u;
+                            uint64_t saved;
+                            asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %1\n\ts_nop 1\n\t"
+                                         "ds_write2_b32 %2, %3, %4 offset1:1\n\ts_mov_b64 exec, %0"
+                                         : "=&s"(saved) : "s"(m), "v"(la), "v"(jb + (uint32_t)(L * 256 + q)), "v"(__float_as_uint(vq[q]))
+                                         : "memory");
+                        } else if (PROBE != 2 && f) {
+#if FLC_DS_W2
+                            // slot = min(cnt, GCAP) + candidates in lower lanes (< GCAP + 64): exact
+                            // while the item fits; past GCAP the item overflows (its row is folded
+                            // dense) and the writes land in the spare slots.  The scalar part is folded
+                            // into the wave's LDS address in SALU (sla), the lane part is one mbcnt
+                            // pair; index and x go out as one ds_write2_b32 (no register pair to
+                            // assemble for a 64-bit store).
+                            const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            uint32_t sb = sla + min(cnt, (uint32_t)GCAP) * 8u;
+                            asm volatile("" : "+s"(sb));             // stays a scalar term: one v_lshl_add
+                            const uint32_t la = sb + pre * 8u;
+                            asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(jb + (uint32_t)(L * 256 + q)),
+                                         "v"(__float_as_uint(vq[q])) : "memory");
+#else
+                            const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, cnt)) & (GCAP - 1);
+                            sg[pos] = make_uint2(jb + (uint32_t)(L * 256 + q), __float_as_uint(vq[q]));
+#endif
+                        }
+                        cnt += (uint32_t)__popcll(m);
+                    }
+                    // keep the norm's fma chain here: left alone, the compiler sinks all 128 of an
+                    // item's fmas to its end and holds the 128 x values live (218 VGPRs)
+                    asm volatile("" : "+v"(a2));
+                }
             }
             rs = rsn;
+            ru = run;
         }
         a2 = wave_sum(a2);                                   // fixed butterfly: deterministic
         const bool fits = cnt <= GCAP;
@@ -352,9 +439,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS_WPE)
                 const uint2 en = v ? sg[e] : make_uint2(0u, 0u);
                 const float x = __uint_as_float(en.y), ax = fabsf(x);
                 const uint32_t loc = en.x & 0x1FFFu;
-                const uint32_t hi8 = ds_hi8(j0 + loc, rk);
-                const uint32_t h24 = (hi8 << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);   // h >> 8
-                const float hf = (float)h24 * 0x1p-24f, hfu = (float)(h24 + 1u) * 0x1p-24f;
+                uint32_t hi8 = 0;
+                float hf, hfu;                                      // hf <= draw / 2^32 (u) <= hfu
+                if constexpr (COMPAT) {
+                    const float ud = v ? sgf[e] : 0.f;
+                    hf = ud;
+                    hfu = __uint_as_float(__float_as_uint(ud) + 1u);
+                } else {
+                    hi8 = ds_hi8(j0 + loc, rk);
+                    const uint32_t h24 = (hi8 << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);   // h >> 8
+                    hf = (float)h24 * 0x1p-24f;
+                    hfu = (float)(h24 + 1u) * 0x1p-24f;
+                }
                 const bool inl = ax * q0 <= 1.0f - 0x1p-18f;
                 const bool nz = v && !(x == 0.f);
                 const bool sure = nz && inl && fmaf(ax, q1, hf) >= 1.0f + 0x1p-20f;
@@ -484,7 +580,10 @@ struct DsLev {
     float v;
     int idx;
 };
-__device__ inline DsLev ds_level(float x, uint32_t j, uint32_t hi8, const DsRow& r, const float4* tab, int s, float sf) {
+// COMPAT: the draw is the caller's float64 uniform ud, against p = p2 * 2^-32 as DitherOp<.., true>.
+template <bool COMPAT>
+__device__ inline DsLev ds_level(float x, uint32_t j, uint32_t hi8, double ud, const DsRow& r, const float4* tab, int s,
+                                 float sf) {
     const float ax = fabsf(x);
     FastDiv dn;
     dn.b = r.n; dn.rb = r.rn; dn.ok = true;
@@ -512,15 +611,20 @@ __device__ inline DsLev ds_level(float x, uint32_t j, uint32_t hi8, const DsRow&
     if (__builtin_expect(__ballot(gap_slow) != 0ull, 0)) {
         if (gap_slow) p2 = num / t.z;
     }
-    uint32_t thr;
-    asm("v_cvt_u32_f32 %0, %1" : "=v"(thr) : "v"(ceilf(p2)));   // saturating: thr32(p)
-    // draw h = hi8 << 24 | lo24 against thr: the top byte decides unless it equals thr's (1 in
-    // 256), so the low hash is computed only for those lanes
-    const uint32_t th = thr >> 24;
-    bool down = hi8 < th;
-    const bool tie = hi8 == th;
-    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
-        if (tie) down = ((hi8 << 24) | (fmix32(colbase(j) + r.rk2) >> 8)) < thr;
+    bool down;
+    if constexpr (COMPAT) {
+        down = ud < (double)ldexpf(p2, -32);
+    } else {
+        uint32_t thr;
+        asm("v_cvt_u32_f32 %0, %1" : "=v"(thr) : "v"(ceilf(p2)));   // saturating: thr32(p)
+        // draw h = hi8 << 24 | lo24 against thr: the top byte decides unless it equals thr's (1 in
+        // 256), so the low hash is computed only for those lanes
+        const uint32_t th = thr >> 24;
+        down = hi8 < th;
+        const bool tie = hi8 == th;
+        if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
+            if (tie) down = ((hi8 << 24) | (fmix32(colbase(j) + r.rk2) >> 8)) < thr;
+        }
     }
     DsLev l;
     l.v = in ? (down ? t.x : t.y) : 0.f;
@@ -529,8 +633,10 @@ __device__ inline DsLev ds_level(float x, uint32_t j, uint32_t hi8, const DsRow&
 }
 
 // C(x)_j: (lev * sign(x)) * pnorm
-__device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow& r, const float4* tab, int s, float sf) {
-    const DsLev l = ds_level(x, j, hi8, r, tab, s, sf);
+template <bool COMPAT>
+__device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, double ud, const DsRow& r, const float4* tab, int s,
+                                  float sf) {
+    const DsLev l = ds_level<COMPAT>(x, j, hi8, ud, r, tab, s, sf);
     return (x == 0.f) ? 0.f : copysignf(l.v, x) * r.n;
 }
 
@@ -543,8 +649,9 @@ __device__ inline float ds_encode(float x, uint32_t j, uint32_t hi8, const DsRow
 // inside one row's list is free, its columns are distinct), the counts into cntr.  A level above
 // DS_MAXLEV or a full half region turns the row dense.
 // ------------------------------------------------------------------------------------------
+template <bool COMPAT>
 __global__ __launch_bounds__(256) void k_ds_resolve(int64_t n, int64_t r0, int64_t rn, DsWs ws,
-                                                    const float* __restrict__ levels, int s) {
+                                                    const float* __restrict__ levels, int s, UniformSrc us) {
     constexpr int NH = DS_NH;
     __shared__ __attribute__((aligned(16))) float4 tab[DS_MAXS];
     __shared__ uint32_t pre[4][65], irow[4][64], igi[4][64], ikey[4][64], imode[4][64], cs[4][64][NH], cr[4][64][NH];
@@ -633,7 +740,10 @@ __global__ __launch_bounds__(256) void k_ds_resolve(int64_t n, int64_t r0, int64
             rr.rn = irpn[wv][k];
             rr.rk2 = ikey[wv][k];
             rr.fast = (imode[wv][k] & DS_FAST) != 0u;
-            const DsLev l = ds_level(x, gk * (uint32_t)(DS_FGS * CHUNK) + loc, en.x >> 13, rr, tab, s, sf);
+            const uint32_t j = gk * (uint32_t)(DS_FGS * CHUNK) + loc;
+            double ud = 0.0;                                  // compat: the element's uniform
+            if constexpr (COMPAT) ud = us.u[(tv ? rk_ : 0) * us.uld + (tv ? j : 0u)];
+            const DsLev l = ds_level<COMPAT>(x, j, en.x >> 13, ud, rr, tab, s, sf);
             const bool keep = tv && !(x == 0.f) && l.idx > 0 && !(l.v == 0.f);
             if (keep) {
                 const uint32_t u = loc >> 11;
@@ -693,11 +803,11 @@ __device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r
 // Folds rows [r0, r0 + rn) into the running sums: the first group starts the tiles at -0, the others
 // continue from `part` (the previous group's tiles); the last group resolves untouched columns
 // over ALL n rows and writes out = sums / wt, the others write their tiles back to `part`.
-template <bool W, int AP>
+template <bool W, int AP, bool COMPAT>
 __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
                                                   int64_t d, DsWs ws, const float* __restrict__ levels, int s,
                                                   const float* __restrict__ w, float wt, float* __restrict__ part,
-                                                  float* __restrict__ out) {
+                                                  float* __restrict__ out, UniformSrc us) {
     static_assert(64 % AP == 0, "row groups tile the 64-row batch");
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     __shared__ __attribute__((aligned(16))) float tile[4][HCHUNK];
@@ -793,7 +903,9 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
                             for (int k = 0; k < HCHUNK / 64; ++k) {
                                 const uint32_t e = (uint32_t)(k * 64 + lane);
                                 if (e < (uint32_t)len) {
-                                    const float ev = ds_encode(rp[e], hbase + e, ds_hi8(hbase + e, rk), rr, tab, s, sf);
+                                    const uint32_t j = hbase + e;
+                                    const float ev = COMPAT ? ds_encode<true>(rp[e], j, 0u, us.u[row * us.uld + j], rr, tab, s, sf)
+                                                            : ds_encode<false>(rp[e], j, ds_hi8(j, rk), 0.0, rr, tab, s, sf);
                                     add(e, W ? wi * ev : ev);
                                 }
                             }
@@ -852,10 +964,11 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
 // Filter grid.  The product build always takes the default; a -DFLC_TUNING build reads the
 // A/B switches once per process (FLC_DS_GRID=res launches a resident-only grid; FLC_DS_GRIDPCT=p
 // caps it at p % of the resident blocks when row groups run).
-struct DsVariant { bool resident; int gridpct; int probe; int64_t rb; };
+struct DsVariant { bool resident; int gridpct; int probe; int64_t rb; int cring; };
 static const DsVariant& ds_variant() {
     static const DsVariant v = [] {
-        DsVariant r{false, 100, 0, DS_RB};
+        DsVariant r{false, 100, 0, DS_RB, DS_RINGC};
+        if (const char* e = tuning_env("FLC_DS_CRING")) r.cring = atoi(e);
         if (const char* e = tuning_env("FLC_DS_RB")) r.rb = std::max<int64_t>(1, atoll(e));
         if (const char* e = tuning_env("FLC_DS_PROBE")) r.probe = atoi(e);
         if (const char* e = tuning_env("FLC_DS_GRIDPCT")) r.gridpct = std::max(10, std::min(100, atoi(e)));
@@ -901,7 +1014,6 @@ static DsWs carve_ds(void* base, int64_t n, int64_t d, size_t* bytes) {
 
 bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d) {
     if (prm->codec != FLC_STD_DITHERING || prm->norm != FLC_NORM_L2) return false;
-    if (pat && pat->d_uniforms) return false;                    // compat draws: dense path
     if (prm->s < 1 || prm->s > DS_MAXS - 1 || !prm->d_levels || n < 1 || d < 1) return false;
     if (d >= (int64_t)0x7FFFFFFF) return false;
     const int m = prm->flags & FLC_PATH_MASK;
@@ -928,6 +1040,13 @@ std::mutex g_ds_mu;
 std::map<int, DsCtx> g_ds_ctx;
 }  // namespace
 
+// Row groups whose norm + resolve overlap the next group's filter (one fold at the end): tuning
+// builds FLC_DS_TAILOV=g, else 1
+static int tail_groups(int64_t n) {
+    static const int g = [] { const char* e = tuning_env("FLC_DS_TAILOV"); return e ? std::max(1, atoi(e)) : 1; }();
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, n));
+}
+
 // Row groups of the fold pipeline: the caller's hint (FLC_ROW_GROUPS(g) in flags), else 1
 // (measured: folds beside an unrestricted filter are starved, K = 2..8 no faster than 1).
 static int ds_groups(const flc_codec_params* prm, int64_t n) {
@@ -945,11 +1064,18 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     const int64_t client0 = pat ? pat->client0 : 0;
     const int64_t H = nhalves(d);
     const int K = ds_groups(prm, n);
+    // compat: the caller's float64 uniforms (the reference's numpy stream) instead of device draws
+    const bool compat = pat && pat->d_uniforms;
+    const UniformSrc us{compat ? pat->d_uniforms : nullptr, (pat && pat->uniforms_ld) ? pat->uniforms_ld : d};
 
-    auto filter = [&](int64_t r0, int64_t rn) -> int {
-        auto kern = v.probe == 1 ? k_ds_filter<16, DS_GCAP, 1> : v.probe == 2 ? k_ds_filter<16, DS_GCAP, 2>
+    hipEvent_t filt_ev = nullptr;
+    auto filter = [&](int64_t r0, int64_t rn, hipStream_t s2 = nullptr) -> int {
+        // s2: the row group's norm / resolve go to this stream (after an event on st), under the
+        // next group's filter
+        auto kern = compat ? (v.cring == 8 ? k_ds_filter<8, DS_GCAP, 0, true> : k_ds_filter<DS_RINGC, DS_GCAP, 0, true>)
+                  : v.probe == 1 ? k_ds_filter<16, DS_GCAP, 1> : v.probe == 2 ? k_ds_filter<16, DS_GCAP, 2>
                   : v.probe == 3 ? k_ds_filter<16, DS_GCAP, 3> : v.probe == 4 ? k_ds_filter<16, DS_GCAP, 4>
-                  : k_ds_filter<16, DS_GCAP>;
+                  : v.probe == 5 ? k_ds_filter<16, DS_GCAP, 5> : k_ds_filter<16, DS_GCAP>;
         int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
         if (v.resident || (K > 1 && v.gridpct < 100)) {
             int per = 0, dev = 0, cus = 0;
@@ -959,23 +1085,30 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
                 gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
         }
         { ProfScope _ps("k_ds_filter", st);
-        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, std::min<int64_t>(v.rb, rn), d, ws); }
+        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, std::min<int64_t>(v.rb, rn), d, ws, us); }
         FLC_CHECK_LAUNCH("k_ds_filter");
-        hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((rn + 3) / 4)), dim3(256), 0, st, r0, rn, ws, w, pnorm_out);
+        hipStream_t sr = st;
+        if (s2) {
+            FLC_CHECK_HIP(hipEventRecord(filt_ev, st));
+            FLC_CHECK_HIP(hipStreamWaitEvent(s2, filt_ev, 0));
+            sr = s2;
+        }
+        hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((rn + 3) / 4)), dim3(256), 0, sr, r0, rn, ws, w, pnorm_out);
         FLC_CHECK_LAUNCH("k_ds_final");
         const int rb = (int)std::max<int64_t>(1, std::min<int64_t>(((rn + 63) / 64 * ws.G + 3) / 4, 8192));
-        { ProfScope _ps("k_ds_resolve", st);
-        hipLaunchKernelGGL(k_ds_resolve, dim3(rb), dim3(256), 0, st, n, r0, rn, ws, prm->d_levels, prm->s); }
+        { ProfScope _ps("k_ds_resolve", sr);
+        hipLaunchKernelGGL(compat ? k_ds_resolve<true> : k_ds_resolve<false>, dim3(rb), dim3(256), 0, sr, n, r0, rn, ws,
+                           prm->d_levels, prm->s, us); }
         FLC_CHECK_LAUNCH("k_ds_resolve");
         return FLC_OK;
     };
     auto accum = [&](int64_t r0, int64_t rn, int first, int last, hipStream_t s2) -> int {
         const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + 3) / 4, 8192));
         ProfScope _ps("k_ds_accum", s2);
-        if (w) hipLaunchKernelGGL((k_ds_accum<true, DS_AP>), dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d,
-                                  ws, prm->d_levels, prm->s, w, wt, ws.part, out);
-        else hipLaunchKernelGGL((k_ds_accum<false, DS_AP>), dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d,
-                                ws, prm->d_levels, prm->s, w, wt, ws.part, out);
+        auto kern = w ? (compat ? k_ds_accum<true, DS_AP, true> : k_ds_accum<true, DS_AP, false>)
+                      : (compat ? k_ds_accum<false, DS_AP, true> : k_ds_accum<false, DS_AP, false>);
+        hipLaunchKernelGGL(kern, dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels, prm->s, w,
+                           wt, ws.part, out, us);
         FLC_CHECK_LAUNCH("k_ds_accum");
         return FLC_OK;
     };
@@ -983,7 +1116,8 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     { ProfScope _ps("k_ds_sample", st);
     hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->seed, client0, ws); }
     FLC_CHECK_LAUNCH("k_ds_sample");
-    if (K == 1) {
+    const int TO = tail_groups(n);
+    if (K == 1 && TO <= 1) {
         int rc = filter(0, n);
         if (rc) return rc;
         return accum(0, n, 1, 1, st);
@@ -1001,10 +1135,24 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         FLC_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         FLC_CHECK_HIP(hipStreamCreateWithPriority(&cx.side, hipStreamNonBlocking, hi));
     }
-    while ((int)cx.ev.size() < K + 1) {
+    while ((int)cx.ev.size() < std::max(K, TO) + 2) {
         hipEvent_t e;
         FLC_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         cx.ev.push_back(e);
+    }
+    if (K == 1) {
+        // Tail overlap: row group g's norm and resolve (latency-bound, little memory traffic) run on
+        // the side stream under the filter of group g + 1; one fold of all rows at the end.
+        // (A stream's events are reused in order: a record after the wait that consumed it.)
+        for (int g = 0; g < TO; ++g) {
+            const int64_t r0 = n * g / TO, r1 = n * (g + 1) / TO;
+            filt_ev = cx.ev[g];
+            int rc = filter(r0, r1 - r0, cx.side);
+            if (rc) return rc;
+        }
+        FLC_CHECK_HIP(hipEventRecord(cx.ev[TO], cx.side));
+        FLC_CHECK_HIP(hipStreamWaitEvent(st, cx.ev[TO], 0));
+        return accum(0, n, 1, 1, st);
     }
     for (int g = 0; g < K; ++g) {
         const int64_t r0 = n * g / K, r1 = n * (g + 1) / K;

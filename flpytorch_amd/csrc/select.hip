@@ -29,6 +29,10 @@
 // Keys: |x| bits with the sign cleared (uint32, monotone; NaN above inf like torch.topk).
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "chunks.hpp"
 #include "randk_tree.hpp"
 
@@ -222,10 +226,10 @@ __device__ inline float4 cs_ld(const float4* p) {
 #endif
 }
 template <int NT>
-__global__ __launch_bounds__(NT) void k_cand_select(int64_t n, int64_t K, SelWs ws) {
+__global__ __launch_bounds__(NT) void k_cand_select(int64_t r0, int64_t rn, int64_t K, SelWs ws) {
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
-    for (int64_t row = blockIdx.x; row < n; row += gridDim.x) {
+    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
         if (ws.flags[row]) continue;                                     // overflowed in the filter
         const uint32_t cnt = ws.rowcnt[(row) * RCS];
         if (cnt < (uint32_t)K) {                                          // sample threshold too high
@@ -576,7 +580,7 @@ template <int RING, int FGS>
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t rb, int64_t d, SelWs ws, int shards) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, SelWs ws, int shards) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     // staging per (buffer, wave): GCAP + 64 indices then GCAP + 64 values (one ds_write2st64_b32
     // per entry; the 64 spare slots take a wave-instruction starting at GCAP, i.e. an overflow)
@@ -587,7 +591,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
     const int64_t C = nchunks(d);
     const int64_t G = (C + FGS - 1) / FGS;                               // groups per row
-    const int64_t items = n * G;
+    const int64_t items = rn * G;                                        // this launch's rows: [r0, r0 + rn)
     const int64_t stride = (int64_t)gridDim.x * 4;
     int64_t it = (int64_t)blockIdx.x * 4 + wv;
     if (it >= items) return;
@@ -596,9 +600,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
     // row-major)
     auto item_at = [&](int64_t t, int64_t& r, int64_t& cc) {
         const int64_t blk = t / (rb * G), rem = t - blk * rb * G;
-        const int64_t bn = min(rb, n - blk * rb);
+        const int64_t bn = min(rb, rn - blk * rb);
         const int64_t g = rem / bn;
-        r = blk * rb + (rem - g * bn);
+        r = r0 + blk * rb + (rem - g * bn);
         cc = g * FGS;
     };
     int64_t row, c;                                                      // current row, chunk
@@ -859,13 +863,13 @@ __device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [EX_NT / 64
 }
 
 template <bool VEC>
-__global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws) {
+__global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, int64_t K, SelWs ws) {
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
     __shared__ uint32_t wsum[EX_NT / 64];
     const int t = threadIdx.x;
     const int64_t C = nchunks(d);
-    for (int64_t row = blockIdx.x; row < n; row += gridDim.x) {
+    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
         if (!(ws.flags[row] & (F_OVERFLOW | F_SHORT))) continue;       // row-uniform
         const float* r = rows.row(row);
         uint32_t prefix = 0, krem = (uint32_t)K;
@@ -1905,18 +1909,35 @@ static int filter_group() {
 }
 
 template <int FGS>
-static void launch_filter(RowSrc rows, int64_t n, int64_t d, SelWs ws, hipStream_t st, int shards) {
+static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, SelWs ws, hipStream_t st,
+                          int shards) {
     // oversubscribed grid (measured: 16-32 K blocks beat a resident-only persistent grid by ~5 %,
     // the hardware dispatcher balances the tail)
-    const int64_t waves = n * ((nchunks(d) + FGS - 1) / FGS);
+    const int64_t waves = rn * ((nchunks(d) + FGS - 1) / FGS);
     const int gw = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 32768));
     static const int64_t rb = [] {
         // rows per block of the item order: 64 measured 0.5 % faster than row-major (1) at C3
         const char* e = tuning_env("FLC_TK_RB");          // tuning runs only
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
-    hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, std::min(rb, std::max<int64_t>(n, 1)), d, ws, shards);
+    hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
+                       std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards);
 }
+
+// Row groups of the TopK fast path whose candidate select + exact fallback run on a side stream
+// under the next group's filter (one fold of all rows at the end): tuning builds FLC_TK_TAILOV=g
+static int tk_tail_groups(int64_t n) {
+    static const int g = [] { const char* e = tuning_env("FLC_TK_TAILOV"); return e ? std::max(1, atoi(e)) : 1; }();
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, n / 64));
+}
+namespace {
+struct TkCtx {
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev;
+};
+std::mutex g_tk_mu;
+std::map<int, TkCtx> g_tk_ctx;
+}  // namespace
 
 static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
                               hipStream_t st);
@@ -2076,36 +2097,68 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
                                few ? 1 : 0); }
             FLC_CHECK_LAUNCH("k_topk_sample");
-            { ProfScope _ps("k_topk_filter", st);
-            // persistent grid: exactly the resident blocks (a second partial wave of blocks would
-            // leave the chip half idle at the end); buffer loads need no 16 B row alignment
-            // few rows: 2-chunk groups (twice the waves in flight for a lone row)
-            // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
-            if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, d, ws, st, few ? CS_SH : 1);
-            else launch_filter<4>(rows, n, d, ws, st, few ? CS_SH : 1); }
-            FLC_CHECK_LAUNCH("k_topk_filter");
-            { ProfScope _ps("k_cand_select", st);
-            // few rows (a lone compressVector): one 1024-thread workgroup per row walks the list 4x wider
-            // many rows: 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
-            // few rows (a lone compressVector): each list over up to 64 workgroups, one launch per
-            // digit (3 cover every shift; a finished row's workgroups exit at once)
-            if (few) {
-                for (int p = 0; p < 3; ++p)
-                    hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws);
-            } else if (n < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)n), dim3(1024), 0, st, n, K, ws);
-            else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(n, 8192)), dim3(512), 0, st, n, K, ws); }
-            FLC_CHECK_LAUNCH("k_cand_select");
+            // per row group: filter (the full read), then the candidate select and the exact
+            // fallback of the group's rows; with TG > 1 groups the select + fallback of group g run
+            // on a side stream under the filter of group g + 1 (both per-row, other rows' lists)
+            const int TG = few ? 1 : tk_tail_groups(n);
+            hipStream_t sside = st;
+            TkCtx* cx = nullptr;
+            std::unique_lock<std::mutex> lk;
+            if (TG > 1) {
+                int dev = 0;
+                FLC_CHECK_HIP(hipGetDevice(&dev));
+                lk = std::unique_lock<std::mutex>(g_tk_mu);
+                cx = &g_tk_ctx[dev];
+                if (!cx->side) {
+                    int lo = 0, hi = 0;
+                    FLC_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                    FLC_CHECK_HIP(hipStreamCreateWithPriority(&cx->side, hipStreamNonBlocking, hi));
+                }
+                while ((int)cx->ev.size() < TG + 1) {
+                    hipEvent_t e;
+                    FLC_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    cx->ev.push_back(e);
+                }
+                sside = cx->side;
+            }
+            for (int g = 0; g < TG; ++g) {
+                const int64_t r0 = n * g / TG, rn = n * (g + 1) / TG - r0;
+                { ProfScope _ps("k_topk_filter", st);
+                // few rows: 2-chunk groups (twice the waves in flight for a lone row)
+                // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
+                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1);
+                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1); }
+                FLC_CHECK_LAUNCH("k_topk_filter");
+                if (TG > 1) {
+                    FLC_CHECK_HIP(hipEventRecord(cx->ev[g], st));
+                    FLC_CHECK_HIP(hipStreamWaitEvent(sside, cx->ev[g], 0));
+                }
+                { ProfScope _ps("k_cand_select", sside);
+                // few rows (a lone compressVector): each list over 64 workgroups, one launch per
+                // digit (3 cover every shift; a finished row's workgroups exit at once); many rows:
+                // 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
+                if (few) {
+                    for (int p = 0; p < 3; ++p)
+                        hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws);
+                } else if (rn < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)rn), dim3(1024), 0, sside, r0, rn, K, ws);
+                else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(rn, 8192)), dim3(512), 0, sside, r0, rn, K, ws); }
+                FLC_CHECK_LAUNCH("k_cand_select");
+                {   // rows the fast path failed (rare): exact selection, one launch
+                    ProfScope _ps("k_topk_exact_rows", sside);
+                    const int eb = grid_stride_blocks(rn, 2048);
+                    if (vec) hipLaunchKernelGGL((k_topk_exact_rows<true>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, r0, rn, d, K, ws);
+                    else hipLaunchKernelGGL((k_topk_exact_rows<false>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, r0, rn, d, K, ws);
+                    FLC_CHECK_LAUNCH("k_topk_exact_rows");
+                }
+            }
+            if (TG > 1) {
+                FLC_CHECK_HIP(hipEventRecord(cx->ev[TG], sside));
+                FLC_CHECK_HIP(hipStreamWaitEvent(st, cx->ev[TG], 0));
+            }
         } else {
             FLC_CHECK_HIP(hipMemsetAsync(ws.flags, 0, (size_t)n * sizeof(uint32_t), st));
         }
-        if (!dense_k) {
-            // rows the fast path failed (rare): exact selection, one launch
-            ProfScope _ps("k_topk_exact_rows", st);
-            const int eb = grid_stride_blocks(n, 2048);
-            if (vec) hipLaunchKernelGGL((k_topk_exact_rows<true>), dim3(eb), dim3(EX_NT), 0, st, rows, n, d, K, ws);
-            else hipLaunchKernelGGL((k_topk_exact_rows<false>), dim3(eb), dim3(EX_NT), 0, st, rows, n, d, K, ws);
-            FLC_CHECK_LAUNCH("k_topk_exact_rows");
-        } else {
+        if (dense_k) {
         // dense K: every row takes the exact multi-launch path
         hipLaunchKernelGGL(k_build_worklist, dim3(1), dim3(1024), 0, st, n, K, d, ws, 1);
         FLC_CHECK_LAUNCH("k_build_worklist");

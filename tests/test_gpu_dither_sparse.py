@@ -1,12 +1,13 @@
 """GPU parity of the sparse fused dithering path (flpytorch_amd/csrc/dither_sparse.hip).
 
-QSGD / standard dithering with p = 2 in device-RNG mode, fused encode + reduce: one pass per row
+QSGD / standard dithering with p = 2, fused encode + reduce: one pass per row
 keeps the elements that could be nonzero (against a sampled lower bound of the norm), the chunk
 owners encode them exactly.  Bar: BIT-EXACT (uint32 compare) against the oracle — the reference's
 op order (oracle/codecs.py, compressors.py:270-299) with the device draws restated in numpy
 (oracle/devrng.py) — including the sign of zero, and bit-identical to the dense two-pass path at
 C4 scale.  Compressor.dither_path = "sparse" | "dense" (the flc_codec_params.flags hint) forces a
-path; the automatic choice keeps small D dense.
+path; the automatic choice keeps small D dense.  Compat mode (the caller's float64 uniforms, the
+reference's numpy stream) takes the same single pass reading the uniforms beside the rows.
 """
 import zlib
 
@@ -45,12 +46,12 @@ def assert_bitexact(got, want):
                              f"{np.asarray(got).ravel()[bad[:5]]} vs {np.asarray(want).ravel()[bad[:5]]}")
 
 
-def oracle_uplink(spec, rows, client0, weights=None, seed=SEED):
+def oracle_uplink(spec, rows, client0, weights=None, seed=SEED, uniforms=None):
     d = rows.shape[1]
     enc, norms = [], []
     for i in range(rows.shape[0]):
         o = oc.OracleCompressor(spec, d)
-        o.testp = devrng.uniforms(seed, client0 + i, d)
+        o.testp = devrng.uniforms(seed, client0 + i, d) if uniforms is None else uniforms[i]
         enc.append(o.compress(rows[i]))
         norms.append(o.norm(rows[i]))
     return oc.reduce_plain(enc, weights), np.array(norms, dtype=np.float32)
@@ -186,7 +187,7 @@ def test_auto_path_choice(ag, monkeypatch):
         try:
             red(x)
             torch.cuda.synchronize()
-            assert _lib.profile_collect(want)[1] == 1, (d, want)
+            assert _lib.profile_collect(want)[1] >= 1, (d, want)     # >= 1: row groups (tuning builds)
             assert _lib.profile_collect(other)[1] == 0, (d, other)
         finally:
             _lib.profile_enable(False)
@@ -210,3 +211,98 @@ def test_sparse_dither_item_near_staging_capacity(ag, monkeypatch, big):
     got = red(torch.from_numpy(rows).cuda(), client0=client0, pnorms_out=pn)
     assert_bitexact(pn, wn)
     assert_bitexact(got, want)
+
+
+def compat_uniforms(n, d, g):
+    """float64 draws in [0, 1) as numpy's random() makes them, with the edges planted: exact 0,
+    the largest double below 1, and values a few ulps either side of 1/2."""
+    u = g.random((n, d))
+    u[:, 5] = 0.0
+    u[:, 6] = np.nextafter(1.0, 0.0)
+    u[:, 7:11] = 0.5 + np.array([-2, -1, 1, 2]) * 2.0 ** -53
+    return u
+
+
+@pytest.mark.parametrize("kind", ["normal", "heavy", "sparse", "negative", "clustered", "ones", "tiny"])
+@pytest.mark.parametrize("spec", ["qsgd:4", "qsgd:127"])
+def test_sparse_dither_compat_vs_oracle(ag, monkeypatch, kind, spec):
+    """Compat draws (float64 uniforms, resident [N, D], a padded row stride) through the single
+    pass: bit-exact against the oracle's `testp < p` with the same uniforms, norms included."""
+    n, d, client0 = 5, 300_001, 11
+    g = np.random.default_rng(zlib.crc32(f"compat{kind}{spec}".encode()))
+    rows = make_rows(kind, n, d, g)
+    uni = compat_uniforms(n, d, g)
+    want, wn = oracle_uplink(spec, rows, client0, uniforms=uni)
+    red = ag.UplinkReducer(sparse(ag, spec, d))
+    pad = torch.zeros((n, d + 3), dtype=torch.float64, device="cuda")   # uniforms_ld = d + 3
+    pad[:, :d] = torch.from_numpy(uni)
+    pn = torch.empty(n, device="cuda")
+    got = red(torch.from_numpy(rows).cuda(), client0=client0, pnorms_out=pn, uniforms=pad[:, :d])
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)
+
+
+@pytest.mark.parametrize("d", [1, 3, 4097, 8192 * 3 + 5, 16385])
+def test_sparse_dither_compat_shapes_and_weights(ag, monkeypatch, d):
+    """Compat draws at chunk / item / sample boundaries, weighted (negative and zero weights), and
+    through the pointer-array entry point."""
+    n = 4
+    g = np.random.default_rng(d + 7)
+    rows = g.standard_normal((n, d)).astype(np.float32)
+    rows[2] = -np.abs(rows[2]) * 1e-3
+    uni = g.random((n, d))
+    w = [1.0, -0.5, 0.0, 2.0]
+    want, _ = oracle_uplink("qsgd:16", rows, 0, weights=w, uniforms=uni)
+    red = ag.UplinkReducer(sparse(ag, "qsgd:16", d))
+    ud = torch.from_numpy(uni).cuda()
+    rt = torch.from_numpy(rows).cuda()
+    assert_bitexact(red(rt, weights=w, uniforms=ud), want)
+    assert_bitexact(red([rt[i].clone() for i in range(n)], weights=w, uniforms=ud), want)
+
+
+@pytest.mark.parametrize("groups", [1, 3])
+def test_sparse_dither_compat_row_groups_nonfinite(ag, monkeypatch, groups):
+    """Compat draws through the row-group pipeline, with a NaN row and a clustered (dense-folded)
+    row: the dense fold reads the uniforms too."""
+    n, d = 7, 150_001
+    g = np.random.default_rng(groups + 40)
+    rows = make_rows("normal", n, d, g)
+    rows[2, 99] = np.nan
+    rows[5] = make_rows("clustered", 1, d, g)[0]
+    uni = g.random((n, d))
+    want, wn = oracle_uplink("qsgd:16", rows, 0, uniforms=uni)
+    comp = sparse(ag, "qsgd:16", d)
+    comp.row_groups = groups
+    red = ag.UplinkReducer(comp)
+    pn = torch.empty(n, device="cuda")
+    got = red(torch.from_numpy(rows).cuda(), pnorms_out=pn, uniforms=torch.from_numpy(uni).cuda())
+    torch.cuda.synchronize()
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)
+
+
+def test_sparse_equals_dense_compat_c4_scale(ag, monkeypatch):
+    """C4's row length with compat draws: the single pass and the dense two-pass path agree bit
+    for bit, and the automatic choice takes the single pass."""
+    from flpytorch_amd import _lib
+    n, d = 4, 25_000_000
+    gen = torch.Generator("cuda").manual_seed(9)
+    x = torch.empty((n, d), device="cuda").normal_(generator=gen)
+    uni = torch.empty((n, d), device="cuda", dtype=torch.float64).uniform_(generator=gen)
+    comp = ag.initCompressor("qsgd:127", d)
+    red = ag.UplinkReducer(comp)
+    outs, norms = {}, {}
+    for path in ("auto", "dense"):
+        comp.dither_path = None if path == "auto" else path
+        pn = torch.empty(n, device="cuda")
+        _lib.profile_enable(True)
+        try:
+            outs[path] = red(x, pnorms_out=pn, uniforms=uni).cpu().numpy()
+            launched = _lib.profile_collect("k_ds_filter")[1]
+        finally:
+            _lib.profile_enable(False)
+        assert (launched >= 1) == (path == "auto"), (path, launched)
+        norms[path] = pn.cpu().numpy()
+    assert_bitexact(norms["auto"], norms["dense"])
+    assert_bitexact(outs["auto"], outs["dense"])
+    assert 0 < np.count_nonzero(outs["auto"]) < d
