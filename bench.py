@@ -763,8 +763,9 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             pj = json.load(f)
-        # only the PMC pass of this line's dominant kernel (compat lines run another kernel)
-        if wl["kernel"] in pj.get("kernel", ""):
+        # only the PMC pass of this line's dominant kernel and pattern source (a compat line's
+        # filter also reads the uniforms)
+        if wl["kernel"] in pj.get("kernel", "") and bool(pj.get("compat")) == bool(args.compat):
             traffic = pj.get("hbm_bytes_per_launch")
 
     if rank == 0:

@@ -73,10 +73,9 @@ struct SelWs {            // carved from the caller workspace
 // ------------------------------------------------------------------------------------------
 // Find, scanning a 2048-bin histogram from the TOP bin down, the bin b where the running count
 // reaches k (1-based).  Returns b and the count strictly above b.  256 threads, 8 bins each.
-__device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
-                                 uint32_t* scratch /* LDS 256+2 */) {
-    const int t = threadIdx.x;
-    const bool own = t < 256;                              // larger blocks: the rest only sync
+// (t, own): the thread's index in the 256 that scan; every thread of the block takes the barriers.
+__device__ inline void hist_find_at(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
+                                    uint32_t* scratch /* LDS 256+2 */, int t, bool own) {
     // thread t owns bins [HBINS-8(t+1), HBINS-8t)  (top bins first)
     uint32_t local[8];
     uint32_t s = 0;
@@ -110,6 +109,21 @@ __device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, u
     above = scratch[257];
     __syncthreads();
 }
+__device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
+                                 uint32_t* scratch /* LDS 256+2 */) {
+    hist_find_at(h, k, bin, above, scratch, (int)threadIdx.x, threadIdx.x < 256);   // larger blocks: the rest only sync
+}
+// Two searches side by side (blocks of >= 512 threads): threads 0-255 scan ha for ka, 256-511 hb for kb.
+__device__ inline void hist_find2(const uint32_t* ha, uint32_t ka, uint32_t& bina, uint32_t& abovea, uint32_t* sa,
+                                  const uint32_t* hb, uint32_t kb, uint32_t& binb, uint32_t& aboveb, uint32_t* sb) {
+    const bool second = threadIdx.x >= 256;
+    uint32_t bin, above;
+    hist_find_at(second ? hb : ha, second ? kb : ka, bin, above, second ? sb : sa, (int)(threadIdx.x & 255u),
+                 threadIdx.x < 512);
+    bina = sa[256]; abovea = sa[257];
+    binb = sb[256]; aboveb = sb[257];
+    __syncthreads();
+}
 
 // pass p: 0 -> bits [30:20], 1 -> [19:9], 2 -> [8:0]
 __device__ inline uint32_t pass_shift(int p) { return p == 0 ? 20u : (p == 1 ? 9u : 0u); }
@@ -127,11 +141,13 @@ __device__ inline uint32_t key_bin(uint32_t key, int p) {
 // ------------------------------------------------------------------------------------------
 // TopK: sample threshold (one workgroup per row)
 // ------------------------------------------------------------------------------------------
-template <int NT>
+// DUAL (few rows: latency-bound): the two rank searches share their passes over the sample; the
+// second histogram costs 8 KB of LDS, which would halve the workgroups per CU of a many-row launch.
+template <int NT, bool DUAL>
 __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few) {
     __shared__ uint32_t keys[SMAX];
-    __shared__ uint32_t h[HBINS];
-    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t h[HBINS], h2[DUAL ? HBINS : 1];
+    __shared__ uint32_t scratch[260], scratch2[DUAL ? 260 : 1];
     const int64_t row = blockIdx.x;
     if (row >= n) return;
     const float* r = rows.row(row);
@@ -165,7 +181,10 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
         double rr = ks + 4.0 * sqrt(ks) + 8.0;
         rank = (uint32_t)min((double)S, ceil(rr));
     }
-    // key of sample rank r (from the top): three 11/11/9-bit passes over the LDS sample
+    // keys of sample ranks ra and rb (from the top) together: three 11/11/9-bit passes over the LDS
+    // sample, one histogram while the two prefixes agree (always in the first pass), the two
+    // searches side by side
+    static_assert(!DUAL || NT >= 512, "hist_find2 takes 512 threads");
     auto rank_key = [&](uint32_t r) {
         uint32_t prefix = 0, krem = r;
         for (int p = 0; p < 3; ++p) {
@@ -184,10 +203,37 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
         }
         return prefix;
     };
-    const uint32_t tkey = rank_key(rank);
-    // estimate of the K-th key (sample rank ks): sizes the first digit of k_cand_select
-    const uint32_t kest = (S == d) ? tkey
-                                   : rank_key((uint32_t)max(1.0, min((double)S, (double)K * (double)S / (double)d)));
+    auto rank_keys = [&](uint32_t ra, uint32_t rb, uint32_t& ka, uint32_t& kb) {
+        if constexpr (!DUAL) {
+            ka = rank_key(ra);
+            kb = rb == ra ? ka : rank_key(rb);
+            return;
+        }
+        uint32_t pa = 0, pb = 0, ma = ra, mb = rb;
+        for (int p = 0; p < 3; ++p) {
+            const bool same = pa == pb;
+            for (int i = threadIdx.x; i < HBINS; i += NT) { h[i] = 0; h2[i] = 0; }
+            __syncthreads();
+            for (int i = threadIdx.x; i < S; i += NT) {
+                const uint32_t k = keys[i];
+                if (key_in_prefix(k, p, pa)) atomicAdd(&h[key_bin(k, p)], 1u);
+                if (!same && key_in_prefix(k, p, pb)) atomicAdd(&h2[key_bin(k, p)], 1u);
+            }
+            __syncthreads();
+            uint32_t ba, aa, bb, ab;
+            hist_find2(h, ma, ba, aa, scratch, same ? h : h2, mb, bb, ab, scratch2);
+            pa = (pa << pass_bits(p)) | ba;
+            ma -= aa;
+            pb = (pb << pass_bits(p)) | bb;
+            mb -= ab;
+        }
+        ka = pa;
+        kb = pb;
+    };
+    // the threshold key (rank), and the estimate of the K-th key (sample rank ks) that sizes the
+    // first digit of k_cand_select
+    uint32_t tkey, kest;
+    rank_keys(rank, S == d ? rank : (uint32_t)max(1.0, min((double)S, (double)K * (double)S / (double)d)), tkey, kest);
     if (threadIdx.x == 0) {
         ws.thr[row] = (rank >= (uint32_t)S && S != d) ? 0u : tkey;
         ws.prefix[row] = kest;
@@ -1925,9 +1971,13 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
 }
 
 // Row groups of the TopK fast path whose candidate select + exact fallback run on a side stream
-// under the next group's filter (one fold of all rows at the end): tuning builds FLC_TK_TAILOV=g
+// under the next group's filter (one fold of all rows at the end), at least 64 rows each: 4
+// (measured at C3, same box, two runs each: 8.18 ms / step with 1 group, 8.15 with 2, 8.00-8.01
+// with 4, 8.04 with 8; profiles/r03/ab_tailov.txt); tuning builds FLC_TK_TAILOV=g.  (The same
+// overlap of the sparse QSGD norm + resolve lost at C4, 10.20 -> 10.27-10.44 ms: its filter split
+// in groups runs slower; it stays a tuning knob there, FLC_DS_TAILOV.)
 static int tk_tail_groups(int64_t n) {
-    static const int g = [] { const char* e = tuning_env("FLC_TK_TAILOV"); return e ? std::max(1, atoi(e)) : 1; }();
+    static const int g = [] { const char* e = tuning_env("FLC_TK_TAILOV"); return e ? std::max(1, atoi(e)) : 4; }();
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, n / 64));
 }
 namespace {
@@ -2094,7 +2144,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         if (!dense_k) {
             { ProfScope _ps("k_topk_sample", st);
             // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3)
-            hipLaunchKernelGGL(k_topk_sample<1024>, dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
+            hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
                                few ? 1 : 0); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             // per row group: filter (the full read), then the candidate select and the exact

@@ -51,7 +51,7 @@ def test_c4_qsgd127_uplink_full_rows_vs_oracle(ag):
         _lib.profile_collect("k_ds_filter")
         got = red(rows, client0=client0, pnorms_out=pn)
         torch.cuda.synchronize()
-        assert _lib.profile_collect("k_ds_filter")[1] == 1          # the bench's sparse path ran
+        assert _lib.profile_collect("k_ds_filter")[1] >= 1          # the bench's sparse path ran (tuning row groups: more)
     finally:
         _lib.profile_enable(False)
     got = got.cpu().numpy()
