@@ -90,63 +90,95 @@ def load():
             raise ImportError(
                 f"flpytorch_amd: {LIB_PATH} is missing — build it with "
                 "`make -C flpytorch_amd/csrc` (or __graft_entry__.build()); there is no CPU fallback")
-        lib = ctypes.CDLL(LIB_PATH)
-        vp, i64, f32, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_int, ctypes.c_size_t
-        P = ctypes.POINTER
-        lib.flc_version.restype = i32
-        lib.flc_last_error_string.restype = ctypes.c_char_p
-        lib.flc_build_id.restype = ctypes.c_char_p
-        lib.flc_reduce_rows.argtypes = [vp, i64, i64, vp, vp, f32, i32, vp, vp]
-        lib.flc_reduce_matrix.argtypes = [vp, i64, i64, i64, vp, vp, f32, i32, vp, vp]
-        lib.flc_encode_workspace_size.argtypes = [P(FlcCodecParams), i64]
-        lib.flc_encode_workspace_size.restype = sz
-        lib.flc_encode.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, vp, vp, vp, sz, vp]
-        lib.flc_encode_reduce_workspace_size.argtypes = [P(FlcCodecParams), i64, i64]
-        lib.flc_encode_reduce_workspace_size.restype = sz
-        lib.flc_encode_reduce.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, i64, i64, vp, f32, vp, vp,
-                                          vp, sz, vp]
-        lib.flc_encode_shift_workspace_size.argtypes = [P(FlcCodecParams), i64]
-        lib.flc_encode_shift_workspace_size.restype = sz
-        lib.flc_encode_shift.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, vp, i64, f32, vp, vp, f32, vp, vp, vp,
-                                         vp, sz, vp]
-        lib.flc_payload_bytes.argtypes = [P(FlcCodecParams), i64]
-        lib.flc_payload_bytes.restype = i64
-        lib.flc_payload_format.argtypes = [P(FlcCodecParams)]
-        lib.flc_payload_validate.argtypes = [P(FlcCodecParams), vp, i64, i64]
-        lib.flc_pack_workspace_size.argtypes = [P(FlcCodecParams), i64]
-        lib.flc_pack_workspace_size.restype = sz
-        lib.flc_pack.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, vp, sz, vp]
-        lib.flc_unpack.argtypes = [P(FlcCodecParams), vp, i64, vp, vp]
-        lib.flc_unpack_reduce_workspace_size.argtypes = [P(FlcCodecParams), i64, i64]
-        lib.flc_unpack_reduce_workspace_size.restype = sz
-        lib.flc_unpack_reduce.argtypes = [P(FlcCodecParams), vp, i64, vp, i64, i64, vp, f32, vp, vp, sz, vp]
-        lib.flc_combine_workspace_size.argtypes = [vp, i64, i32]
-        lib.flc_combine_workspace_size.restype = sz
-        lib.flc_combine_partials.argtypes = [vp, vp, i64, f32, i32, vp, sz, vp]
-        lib.flc_combine_blocks_workspace_size.argtypes = [vp, i64, i64]
-        lib.flc_combine_blocks_workspace_size.restype = sz
-        lib.flc_combine_blocks.argtypes = [vp, vp, i64, i64, i64, f32, vp, vp, sz, vp]
-        lib.flc_mt_choice.argtypes = [vp, vp, i64, i64, vp, vp]
-        lib.flc_mt_rand.argtypes = [vp, vp, i64, vp]
-        lib.flc_mt_randint31.argtypes = [vp, vp, i64, vp]
-        lib.flc_device_uniform.argtypes = [ctypes.c_uint64, i64, i64]
-        lib.flc_device_uniform.restype = ctypes.c_double
-        lib.flc_device_randk_indices.argtypes = [ctypes.c_uint64, i64, i64, i64, vp]
-        lib.flc_device_randk_counts_workspace_size.argtypes = [i64, i64]
-        lib.flc_device_randk_counts_workspace_size.restype = sz
-        lib.flc_device_randk_counts.argtypes = [ctypes.c_uint64, i64, i64, i64, i64, vp, vp, sz, vp]
-        lib.flc_profile_enable.argtypes = [i32]
-        lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
-        lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
-        for name in EXPORTS:
-            if name not in ("flc_version", "flc_build_id", "flc_last_error_string", "flc_device_uniform",
-                            "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
-                            "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",
-                            "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size",
-                            "flc_combine_blocks_workspace_size", "flc_device_randk_counts_workspace_size"):
-                getattr(lib, name).restype = i32
-        _lib = lib
-        return lib
+        _lib = _bind(ctypes.CDLL(LIB_PATH))
+        return _lib
+
+
+def open_variant(tag):
+    """Another build of the library for an in-process A/B (tools/ab_inproc.py): tag "" or "prod" is
+    the product libflcodec.so, else flpytorch_amd/libflcodec_<tag>.so.  Not cached; make it the one
+    every wrapper calls with ``use(lib)``."""
+    path = os.path.join(_HERE, "libflcodec.so" if tag in ("", "prod") else f"libflcodec_{tag}.so")
+    if not os.path.exists(path):
+        raise ImportError(f"flpytorch_amd: {path} is missing")
+    return _bind(ctypes.CDLL(path))
+
+
+class use:
+    """Context manager: the wrappers call ``lib`` (an open_variant() handle) inside the block."""
+
+    def __init__(self, lib):
+        self.lib, self.prev = lib, None
+
+    def __enter__(self):
+        global _lib
+        load()
+        self.prev, _lib = _lib, self.lib
+        return self.lib
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.prev
+        return False
+
+
+def _bind(lib):
+    """Declare the C ABI's argument and result types on a loaded library."""
+    vp, i64, f32, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_int, ctypes.c_size_t
+    P = ctypes.POINTER
+    lib.flc_version.restype = i32
+    lib.flc_last_error_string.restype = ctypes.c_char_p
+    lib.flc_build_id.restype = ctypes.c_char_p
+    lib.flc_reduce_rows.argtypes = [vp, i64, i64, vp, vp, f32, i32, vp, vp]
+    lib.flc_reduce_matrix.argtypes = [vp, i64, i64, i64, vp, vp, f32, i32, vp, vp]
+    lib.flc_encode_workspace_size.argtypes = [P(FlcCodecParams), i64]
+    lib.flc_encode_workspace_size.restype = sz
+    lib.flc_encode.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, vp, vp, vp, sz, vp]
+    lib.flc_encode_reduce_workspace_size.argtypes = [P(FlcCodecParams), i64, i64]
+    lib.flc_encode_reduce_workspace_size.restype = sz
+    lib.flc_encode_reduce.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, i64, i64, vp, f32, vp, vp,
+                                      vp, sz, vp]
+    lib.flc_encode_shift_workspace_size.argtypes = [P(FlcCodecParams), i64]
+    lib.flc_encode_shift_workspace_size.restype = sz
+    lib.flc_encode_shift.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, vp, i64, f32, vp, vp, f32, vp, vp, vp,
+                                     vp, sz, vp]
+    lib.flc_payload_bytes.argtypes = [P(FlcCodecParams), i64]
+    lib.flc_payload_bytes.restype = i64
+    lib.flc_payload_format.argtypes = [P(FlcCodecParams)]
+    lib.flc_payload_validate.argtypes = [P(FlcCodecParams), vp, i64, i64]
+    lib.flc_pack_workspace_size.argtypes = [P(FlcCodecParams), i64]
+    lib.flc_pack_workspace_size.restype = sz
+    lib.flc_pack.argtypes = [P(FlcCodecParams), P(FlcPattern), vp, i64, vp, vp, sz, vp]
+    lib.flc_unpack.argtypes = [P(FlcCodecParams), vp, i64, vp, vp]
+    lib.flc_unpack_reduce_workspace_size.argtypes = [P(FlcCodecParams), i64, i64]
+    lib.flc_unpack_reduce_workspace_size.restype = sz
+    lib.flc_unpack_reduce.argtypes = [P(FlcCodecParams), vp, i64, vp, i64, i64, vp, f32, vp, vp, sz, vp]
+    lib.flc_combine_workspace_size.argtypes = [vp, i64, i32]
+    lib.flc_combine_workspace_size.restype = sz
+    lib.flc_combine_partials.argtypes = [vp, vp, i64, f32, i32, vp, sz, vp]
+    lib.flc_combine_blocks_workspace_size.argtypes = [vp, i64, i64]
+    lib.flc_combine_blocks_workspace_size.restype = sz
+    lib.flc_combine_blocks.argtypes = [vp, vp, i64, i64, i64, f32, vp, vp, sz, vp]
+    lib.flc_mt_choice.argtypes = [vp, vp, i64, i64, vp, vp]
+    lib.flc_mt_rand.argtypes = [vp, vp, i64, vp]
+    lib.flc_mt_randint31.argtypes = [vp, vp, i64, vp]
+    lib.flc_device_uniform.argtypes = [ctypes.c_uint64, i64, i64]
+    lib.flc_device_uniform.restype = ctypes.c_double
+    lib.flc_device_randk_indices.argtypes = [ctypes.c_uint64, i64, i64, i64, vp]
+    lib.flc_device_randk_counts_workspace_size.argtypes = [i64, i64]
+    lib.flc_device_randk_counts_workspace_size.restype = sz
+    lib.flc_device_randk_counts.argtypes = [ctypes.c_uint64, i64, i64, i64, i64, vp, vp, sz, vp]
+    lib.flc_profile_enable.argtypes = [i32]
+    lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
+    lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
+    for name in EXPORTS:
+        if name not in ("flc_version", "flc_build_id", "flc_last_error_string", "flc_device_uniform",
+                        "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
+                        "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",
+                        "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size",
+                        "flc_combine_blocks_workspace_size", "flc_device_randk_counts_workspace_size"):
+            getattr(lib, name).restype = i32
+    return lib
 
 
 def source_hash(root=None):

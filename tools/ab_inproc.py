@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""In-process A/B of library builds on ONE resident allocation (GPU box).
+
+The rows' physical placement moves a whole step by up to ~10 % from one allocation (one process)
+to the next, which swamps most kernel changes when variants run in separate
+processes.  Here every variant (flpytorch_amd/libflcodec_<tag>.so, "prod" = the product library)
+is loaded into one process (_lib.open_variant / _lib.use) and timed on the same rows, rounds
+interleaved: the per-variant medians compare kernels at matched placement.  Each round also times
+a plain read of the rows (the serverGradient fold) as the allocation's ceiling.
+
+usage: python tools/ab_inproc.py --workload c4 --variants head,prod [--rounds 5] [--steps 5]
+Prints one JSON line per (round, variant) and a summary line per variant.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+WL = {"c3": ("topk:1%", 1024, 10_000_000, ["k_topk_filter", "k_topk_sample", "k_cand_select", "k_chunk_accum"]),
+      "c4": ("qsgd:127", 512, 25_000_000, ["k_ds_filter", "k_ds_sample", "k_ds_resolve", "k_ds_accum"]),
+      "c2": ("randk:1%", 256, 1_000_000, ["k_randk_gen", "k_randk_counts", "k_chunk_accum"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c4", choices=sorted(WL))
+    ap.add_argument("--variants", default="head,prod")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--row-groups", type=int, default=None)
+    a = ap.parse_args()
+    from flpytorch_amd import _lib
+    from flpytorch_amd import aggregation as ag
+    spec, n, d, kernels = WL[a.workload]
+    n = a.n or n
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    gen = torch.Generator(device=dev).manual_seed(1000)
+    rows = torch.empty((n, d), dtype=torch.float32, device=dev)
+    for i in range(0, n, 64):
+        rows[i:i + 64].normal_(generator=gen)
+    out = torch.empty(d, dtype=torch.float32, device=dev)
+    variants = a.variants.split(",")
+    libs = {v: _lib.open_variant(v) for v in variants}
+    comp = ag.initCompressor(spec, d)
+    if a.row_groups:
+        comp.row_groups = a.row_groups
+    red = ag.UplinkReducer(comp, device=dev, seed=20241015)
+    ref = None
+    res = {v: [] for v in variants}
+    for r in range(a.rounds):
+        # the allocation's read ceiling this round (product library)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ag.reduce_rows(out, rows, relative=False, out=out)
+        e0.record()
+        ag.reduce_rows(out, rows, relative=False, out=out)
+        e1.record()
+        e1.synchronize()
+        read_ms = e0.elapsed_time(e1)
+        for v in variants:
+            with _lib.use(libs[v]):
+                red(rows, out=out)                        # warm (and workspace for this build)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.clone()
+                elif not torch.equal(out.view(torch.int32), ref.view(torch.int32)):
+                    raise SystemExit(f"variant {v}: output bits differ from {variants[0]}")
+                _lib.profile_enable(True)
+                for k in kernels:
+                    _lib.profile_collect(k)
+                e0.record()
+                for _ in range(a.steps):
+                    red(rows, out=out)
+                e1.record()
+                e1.synchronize()
+                _lib.profile_enable(False)
+                ks = {}
+                for k in kernels:
+                    ms, cnt = _lib.profile_collect(k)
+                    ks[k] = round(ms / a.steps, 4)
+            step = e0.elapsed_time(e1) / a.steps
+            res[v].append((step, ks))
+            print(json.dumps({"round": r, "variant": v, "ms_per_step": round(step, 4), "read_ms": round(read_ms, 4),
+                              "kernels_ms_per_step": ks}), flush=True)
+    for v in variants:
+        st = [s for s, _ in res[v]]
+        med = {k: round(statistics.median(ks[k] for _, ks in res[v]), 4) for k in kernels}
+        print(json.dumps({"variant": v, "median_ms_per_step": round(statistics.median(st), 4),
+                          "min_ms_per_step": round(min(st), 4), "median_kernels_ms": med}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

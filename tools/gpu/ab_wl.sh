@@ -14,6 +14,7 @@ for wla in ${WLS:-c4 c3}; do
   for rep in 1 2; do
     for va in ${VARIANTS:-head nt}; do
       v=${va%%@*}; ev=""; [ "$va" != "$v" ] && ev=${va#*@}   # "tuning@FLC_DS_RB=16": variant + one env knob
+      [ "$v" = prod ] && v=""                                 # "prod": the product libflcodec.so
       env $ev FLC_LIB_VARIANT=$v timeout -k 10 300 python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline $BENCH_ARGS > $out/run.log 2>&1 || exit $?
       echo "$wla $va $(tail -1 $out/run.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["ms_per_step"], r["kernel_ms_per_step"], r.get("other_kernels_avg_ms"))')" >> $out/ab.log
     done

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 3 (session 2): all GPU tests, then in-process A/B (one allocation) of the lane-per-item
+# resolve + ring fold against the previous build on C4
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+out=gpurun_out/r03s2ab3; mkdir -p $out
+timeout -k 10 600 python -u -m pytest -q -p no:cacheprovider --timeout 120 --timeout-method thread -x tests -m gpu > $out/tests.log 2>&1; rc=$?
+echo "tests rc=$rc $(tail -1 $out/tests.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR|E )" $out/tests.log | head -20; exit 1; }
+timeout -k 10 400 python tools/ab_inproc.py --workload c4 --variants head,prod --rounds 4 > $out/inproc_c4.log 2>&1 || { tail -20 $out/inproc_c4.log; exit 1; }
+tail -2 $out/inproc_c4.log

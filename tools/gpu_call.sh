@@ -3,7 +3,7 @@
 # (box not prepared / no slot free; nothing ran, nothing charged).  A command that ran and failed
 # is never re-submitted.   usage: tools/gpu_call.sh <timeout_s> '<command>'
 t=$1; shift
-for attempt in 1 2 3 4; do
+for attempt in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$@" > /tmp/gpu_call.out 2>&1
   rc=$?
   st=$(python3 -c "import json; print(json.load(open('/root/repo/gpurun_out/.last_call.json'))['status'])" 2>/dev/null)
