@@ -99,6 +99,8 @@ struct DsWs {
     float* rpn;           // [N] RN(1 / norm)
     uint32_t* rk;         // [N] device-RNG row key
     float* part;          // [D] running sums carried between the row groups' folds
+    float4* gtab;         // [DS_MAXS] level table (load_table) for the fold's dense rows, made by
+                          // k_ds_sample: the fold keeps only its tile in LDS
     int64_t cap;          // per row: G * GCAP (each filter item owns a fixed region)
     int64_t G;            // filter items per row
     int64_t n;            // rows
@@ -116,9 +118,10 @@ __device__ inline float f32_down(double v) { float f = (float)v; return (double)
 // Sample: one workgroup per row.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64_t d, const float* __restrict__ levels,
-                                                   uint64_t seed, int64_t client0, DsWs ws) {
+                                                   int s, uint64_t seed, int64_t client0, DsWs ws) {
     __shared__ double r2[4], r4[4];
     const int64_t row = blockIdx.x;
+    if (blockIdx.x == 0) load_table(levels, s, ws.gtab);
     if (row >= n) return;
     const float* r = rows.row(row);
     double a2 = 0.0, a4 = 0.0;
@@ -786,44 +789,50 @@ __device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r
     m.off = 0; m.cnt = 0;
     m.pn = 1.f; m.rpn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
     if (r < rend) {
+        // every load issued at once (no flags -> tab dependency): a dense row's count is dropped below
         m.pn = ws.pn[r];
         m.rpn = ws.rpn[r];
         m.rk = ws.rk[r];
         m.mode = ws.flags[r];
-        if (!(m.mode & DS_DENSE)) {                          // c: half-chunk index
-            const uint2 t = ws.tabs[c * n + r];
-            m.off = t.x;
-            m.cnt = t.y + ws.cntr[c * n + r];
-        }
+        const uint32_t c0 = ws.tabs[c * n + r].y, c1 = ws.cntr[c * n + r];   // c: half-chunk index
+        m.cnt = (m.mode & DS_DENSE) ? 0u : c0 + c1;
         if (w) m.w = w[r];
     }
     return m;
 }
 
+#ifndef FLC_DS_AW
+#define FLC_DS_AW 1                  // waves per fold workgroup (LDS: one 8 KB tile per wave)
+#endif
+constexpr int DS_AW = FLC_DS_AW;
+
 // Folds rows [r0, r0 + rn) into the running sums: the first group starts the tiles at -0, the others
 // continue from `part` (the previous group's tiles); the last group resolves untouched columns
 // over ALL n rows and writes out = sums / wt, the others write their tiles back to `part`.
+// Small workgroups with only the tile in LDS (the dense rows' level table is ws.gtab): up to 19
+// waves per CU for this latency-bound walk (a 4-wave block with the table in LDS fit 3 per CU).
+// The row walk is a ring of AP rows' first 64 entries: row q's slot is refilled with row q + AP
+// as soon as q is folded, so a list load has AP - 1 rows of work in front of it.
 template <bool W, int AP, bool COMPAT>
-__global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
+__global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
                                                   int64_t d, DsWs ws, const float* __restrict__ levels, int s,
                                                   const float* __restrict__ w, float wt, float* __restrict__ part,
                                                   float* __restrict__ out, UniformSrc us) {
     static_assert(64 % AP == 0, "row groups tile the 64-row batch");
     constexpr uint32_t NONE = 0xFFFFFFFFu;
-    __shared__ __attribute__((aligned(16))) float tile[4][HCHUNK];
-    __shared__ __attribute__((aligned(16))) float4 tab[DS_MAXS];
+    __shared__ __attribute__((aligned(16))) float tile[DS_AW][HCHUNK];
     __shared__ float lvl[DS_MAXLEV + 1];
-    load_table(levels, s, tab);
     if (threadIdx.x <= (unsigned)DS_MAXLEV) lvl[threadIdx.x] = (int)threadIdx.x <= s ? levels[threadIdx.x] : 0.f;
     __syncthreads();
+    const float4* tab = ws.gtab;
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = DS_AW == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t H = nhalves(d);
     float* tl = tile[wv];
     const int64_t rend = r0 + rn;
     const int64_t nb = (rn + 63) / 64;
     const float sf = (float)s;
-    for (int64_t h = (int64_t)blockIdx.x * 4 + wv; h < H; h += (int64_t)gridDim.x * 4) {
+    for (int64_t h = (int64_t)blockIdx.x * DS_AW + wv; h < H; h += (int64_t)gridDim.x * DS_AW) {
         // The tile starts at -0.0: (-0) + t == t for every nonzero t, and a column that received a
         // nonzero contribution never returns to -0 (x + y == -0 needs two -0 addends), so a final
         // -0 bit pattern marks exactly the untouched columns.  Zero contributions are not added.
@@ -834,14 +843,13 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
         const int64_t len = min((int64_t)HCHUNK, d - (int64_t)hbase);
         for (int i = lane; i < HCHUNK; i += 64) tl[i] = (first || i >= len) ? -0.f : part[hbase + i];
         DsMeta cur = ds_meta(ws, h, n, rend, r0 + lane, w), nxt;
-        uint32_t ra[AP];                        // ring: first 64 entries of the next AP rows' lists
+        uint32_t ra[AP];                        // ring: first 64 entries of rows q .. q + AP - 1
         // a list's 64-entry window never leaves its item's half region (DS_HCAP >= 64): loaded
         // whole, lanes past the count dropped; an empty list (rows past the end, dense rows) reads
         // the array's first 64 entries instead
         auto fetch = [&](const DsMeta& m, int q, int64_t row, int slot) {
-            const uint32_t off = __builtin_amdgcn_readlane(m.off, q), cnt = __builtin_amdgcn_readlane(m.cnt, q);
+            const uint32_t cnt = __builtin_amdgcn_readlane(m.cnt, q);
             const uint16_t* p = cnt ? ws.ent16 + (h * n + row) * DS_HCAP : ws.ent16;
-            (void)off;
             const uint32_t v = p[lane];
             ra[slot] = (uint32_t)lane < cnt ? v : NONE;
         };
@@ -851,12 +859,18 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
             if (!(t == 0.f)) tl[loc] = tl[loc] + t;
         };
         auto value = [&](uint32_t e, float pn) {            // copysign(levels[lev], sign) * pnorm
-            const float lv = lvl[e >> 12];
+            const float lv = lvl[(e >> 12) & 15u];
             return __uint_as_float(__float_as_uint(lv) | ((e & 0x800u) << 20)) * pn;
         };
         auto row_state = [&](const DsMeta& m, int q, float& pn, float& wi) {
             pn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.pn), q));
             wi = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m.w), q));
+        };
+        // refill the slot of row q (this batch) with row q + AP (past the batch end: the next
+        // batch's meta; past n: empty lists)
+        auto refill = [&](int q, int64_t i0) {
+            if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, q % AP);
+            else fetch(nxt, q + AP - 64, i0 + q + AP, q % AP);   // q % AP: static once unrolled
         };
 #pragma unroll
         for (int q = 0; q < AP; ++q) fetch(cur, q, r0 + q, q);
@@ -865,32 +879,35 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
             nxt = ds_meta(ws, h, n, rend, i0 + 64 + lane, w);
             // rows of this batch that need the general path: dense, or more than 64 entries here
             const uint64_t slow = __ballot((i0 + lane < rend) && ((cur.mode & DS_DENSE) || cur.cnt > 64u));
-            for (int qb = 0; qb < 64; qb += AP) {
-                const int nrow = (int)min((int64_t)AP, rend - (i0 + qb));
-                if (nrow == AP && ((slow >> qb) & ((AP == 64 ? 0ull : (1ull << AP)) - 1ull)) == 0ull) {
-                    // straight line: AP rows' contributions, then the adds in row order
-                    float t[AP];
+            if (slow == 0ull && i0 + 64 <= rend) {
+                // straight line: per row its contribution, the add, the slot's refill
+#pragma unroll 1
+                for (int qb = 0; qb < 64; qb += AP) {
 #pragma unroll
                     for (int u = 0; u < AP; ++u) {
-                        float pn, wi;
-                        row_state(cur, qb + u, pn, wi);
-                        const float e = value(ra[u], pn);
-                        t[u] = W ? wi * e : e;
-                    }
-#pragma unroll
-                    for (int u = 0; u < AP; ++u)
-                        if (ra[u] != NONE) add(ra[u] & (HCHUNK - 1), t[u]);
-                } else {
-                    for (int u = 0; u < nrow; ++u) {
                         const int q = qb + u;
+                        float pn, wi;
+                        row_state(cur, q, pn, wi);
+                        const uint32_t a = ra[u];
+                        const float e = value(a, pn);
+                        if (a != NONE) add(a & (HCHUNK - 1), W ? wi * e : e);
+                        refill(q, i0);
+                    }
+                }
+            } else {
+                const int nrow = (int)min((int64_t)64, rend - i0);
+#pragma unroll 1
+                for (int q = 0; q < 64; ++q) {
+                    const int u = q % AP;
+                    uint32_t a = NONE;
+#pragma unroll
+                    for (int z = 0; z < AP; ++z)
+                        if (z == u) a = ra[z];
+                    if (q < nrow) {
                         const int64_t row = i0 + q;
                         float pn, wi;
                         row_state(cur, q, pn, wi);
                         const uint32_t mode = __builtin_amdgcn_readlane(cur.mode, q);
-                        uint32_t a = NONE;
-#pragma unroll
-                        for (int z = 0; z < AP; ++z)
-                            if (z == u) a = ra[z];
                         if (mode & DS_DENSE) {
                             // dense row: every element of the half chunk, coalesced
                             DsRow rr;
@@ -922,13 +939,16 @@ __global__ __launch_bounds__(256) void k_ds_accum(RowSrc rows, int64_t n, int64_
                             }
                         }
                     }
-                }
-                // refill the slots with rows qb + AP .. (next batch's meta past the batch end)
+                    // refill the slot with row q + AP (dynamic slot: the loop is not unrolled)
+                    const bool nb_ = q + AP >= 64;
+                    const int qq = nb_ ? q + AP - 64 : q + AP;
+                    const uint32_t cnt = __builtin_amdgcn_readlane(nb_ ? nxt.cnt : cur.cnt, qq);
+                    const int64_t rown = i0 + q + AP;
+                    const uint16_t* p = cnt ? ws.ent16 + (h * n + rown) * DS_HCAP : ws.ent16;
+                    const uint32_t v = (uint32_t)lane < cnt ? (uint32_t)p[lane] : NONE;
 #pragma unroll
-                for (int u = 0; u < AP; ++u) {
-                    const int q = qb + u;
-                    if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, u);
-                    else fetch(nxt, q + AP - 64, i0 + q + AP, u);
+                    for (int z = 0; z < AP; ++z)
+                        if (z == u) ra[z] = v;
                 }
             }
             cur = nxt;
@@ -1003,6 +1023,7 @@ static DsWs carve_ds(void* base, int64_t n, int64_t d, size_t* bytes) {
     w.rpn = cv.take<float>(nn);
     w.rk = cv.take<uint32_t>(nn);
     w.part = cv.take<float>((size_t)std::max<int64_t>(d, 1));
+    w.gtab = cv.take<float4>(DS_MAXS);
     if (bytes) *bytes = cv.bytes();
     return w;
 }
@@ -1103,18 +1124,18 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         return FLC_OK;
     };
     auto accum = [&](int64_t r0, int64_t rn, int first, int last, hipStream_t s2) -> int {
-        const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + 3) / 4, 8192));
+        const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + DS_AW - 1) / DS_AW, 32768));
         ProfScope _ps("k_ds_accum", s2);
         auto kern = w ? (compat ? k_ds_accum<true, DS_AP, true> : k_ds_accum<true, DS_AP, false>)
                       : (compat ? k_ds_accum<false, DS_AP, true> : k_ds_accum<false, DS_AP, false>);
-        hipLaunchKernelGGL(kern, dim3(ab), dim3(256), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels, prm->s, w,
+        hipLaunchKernelGGL(kern, dim3(ab), dim3(64 * DS_AW), 0, s2, rows, n, r0, rn, first, last, d, ws, prm->d_levels, prm->s, w,
                            wt, ws.part, out, us);
         FLC_CHECK_LAUNCH("k_ds_accum");
         return FLC_OK;
     };
 
     { ProfScope _ps("k_ds_sample", st);
-    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->seed, client0, ws); }
+    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->s, prm->seed, client0, ws); }
     FLC_CHECK_LAUNCH("k_ds_sample");
     const int TO = tail_groups(n);
     if (K == 1 && TO <= 1) {
