@@ -10,6 +10,10 @@ a plain read of the rows (the serverGradient fold) as the allocation's ceiling.
 
 usage: python tools/ab_inproc.py --workload c4 --variants head,prod [--rounds 5] [--steps 5]
 Prints one JSON line per (round, variant) and a summary line per variant.
+
+Keep it to three builds per process: each build creates its own side streams, a process has four
+hardware queues, and the 4th / 5th build loaded ran every kernel 8-120 % slower in two runs
+(profiles/r03/inproc_ab3.txt, inproc_ab4.txt).
 """
 import argparse
 import json
@@ -48,6 +52,8 @@ def main():
         rows[i:i + 64].normal_(generator=gen)
     out = torch.empty(d, dtype=torch.float32, device=dev)
     variants = a.variants.split(",")
+    if len(variants) > 3:
+        print(f"warning: {len(variants)} builds in one process; more than 3 distorted the timing before", file=sys.stderr)
     libs = {v: _lib.open_variant(v) for v in variants}
     comp = ag.initCompressor(spec, d)
     if a.row_groups:
