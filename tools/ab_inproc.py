@@ -8,7 +8,7 @@ is loaded into one process (_lib.open_variant / _lib.use) and timed on the same 
 interleaved: the per-variant medians compare kernels at matched placement.  Each round also times
 a plain read of the rows (the serverGradient fold) as the allocation's ceiling.
 
-usage: python tools/ab_inproc.py --workload c4 --variants head,prod [--rounds 5] [--steps 5]
+usage: python tools/ab_inproc.py --workload c4 --variants head,prod[,prod:rg4] [--rounds 5] [--steps 5]
 Prints one JSON line per (round, variant) and a summary line per variant.
 
 Keep it to three builds per process: each build creates its own side streams, a process has four
@@ -51,14 +51,20 @@ def main():
     for i in range(0, n, 64):
         rows[i:i + 64].normal_(generator=gen)
     out = torch.empty(d, dtype=torch.float32, device=dev)
+    # a variant is "<build>" or "<build>:rg<K>" (the same build with the row-group hint K)
     variants = a.variants.split(",")
-    if len(variants) > 3:
-        print(f"warning: {len(variants)} builds in one process; more than 3 distorted the timing before", file=sys.stderr)
-    libs = {v: _lib.open_variant(v) for v in variants}
-    comp = ag.initCompressor(spec, d)
-    if a.row_groups:
-        comp.row_groups = a.row_groups
-    red = ag.UplinkReducer(comp, device=dev, seed=20241015)
+    builds = sorted({v.split(":")[0] for v in variants})
+    if len(builds) > 3:
+        print(f"warning: {len(builds)} builds in one process; more than 3 distorted the timing before", file=sys.stderr)
+    blibs = {b: _lib.open_variant(b) for b in builds}
+    libs = {v: blibs[v.split(":")[0]] for v in variants}
+    reds = {}
+    for v in variants:
+        comp = ag.initCompressor(spec, d)
+        rg = int(v.split(":rg")[1]) if ":rg" in v else a.row_groups
+        if rg:
+            comp.row_groups = rg
+        reds[v] = ag.UplinkReducer(comp, device=dev, seed=20241015)
     ref = None
     res = {v: [] for v in variants}
     for r in range(a.rounds):
@@ -71,6 +77,7 @@ def main():
         e1.synchronize()
         read_ms = e0.elapsed_time(e1)
         for v in variants:
+            red = reds[v]
             with _lib.use(libs[v]):
                 red(rows, out=out)                        # warm (and workspace for this build)
                 torch.cuda.synchronize()
