@@ -466,7 +466,8 @@ def dropin(args):
         res[name] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
     # per-kernel device time of one compressVector (flc_profile scopes)
     kernels = ["k_topk_sample", "k_topk_filter", "k_cand_select", "k_topk_exact_rows", "k_chunk_accum",
-               "k_norm_partials", "k_ew_accum_vec", "k_ew_encode", "k_randk_scatter_dev", "k_assign_scatter"]
+               "k_norm_partials", "k_ew_accum_vec", "k_ew_encode", "k_randk_scatter_dev", "k_assign_scatter",
+               "k_assign_finish"]
     _lib.profile_enable(True)
     for k in kernels:
         _lib.profile_collect(k)

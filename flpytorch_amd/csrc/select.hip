@@ -619,14 +619,17 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 // loads deep (the next chunk's descriptor is built up front; past the last item it has
 // num_records 0 and its loads return zeros without touching memory).
 // FGS: chunks per work item (group).
-template <int RING, int FGS>
+template <int RING, int FGS, bool ZF = false>
 #ifndef FLC_TK_RING
 #define FLC_TK_RING 16               // loads in flight per wave (ring registers: 4 x RING VGPRs)
 #endif
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, SelWs ws, int shards) {
+// ZF (a lone compressVector row): every float4 read is also written as zeros to zout, the dense
+// output the selected entries are then scattered into (no separate fill of the output).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, SelWs ws, int shards,
+                                                                                                float* __restrict__ zout) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     // staging per (buffer, wave): GCAP + 64 indices then GCAP + 64 values (one ds_write2st64_b32
     // per entry; the 64 spare slots take a wave-instruction starting at GCAP, i.e. an overflow)
@@ -732,6 +735,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
             }
             const uint32_t cnt0 = cnt;
+            __amdgpu_buffer_rsrc_t ro;
+            if constexpr (ZF) ro = chunk_rsrc(zout, j0, d);
             // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
             // component) index constants out of the loop into 64 live VGPRs
             uint32_t lb = (uint32_t)j0 + (uint32_t)lane * 4u;   // row index of the lane's element 0
@@ -741,6 +746,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 const int P = L + RING - 1;
                 ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
                 const float4 x = ring[L % RING];
+                if constexpr (ZF) {
+                    // unconditional (range-checked): one more store per step in the vmcnt queue
+                    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+                    const u4v z = {0u, 0u, 0u, 0u};
+                    __builtin_amdgcn_raw_buffer_store_b128(z, ro, lane * 16, L * 1024, 0);
+                }
                 const uint32_t jl = lb + (uint32_t)(L * 256);             // index in the row
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -908,15 +919,14 @@ __device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [EX_NT / 64
     return before + inc - v;
 }
 
+// One row's exact selection by one EX_NT-thread workgroup: three radix passes over the row, then the
+// row's list rewritten with exactly its admitted entries in index order (ties: the lowest indices).
 template <bool VEC>
-__global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, int64_t K, SelWs ws) {
-    __shared__ uint32_t h[HBINS];
-    __shared__ uint32_t scratch[260];
-    __shared__ uint32_t wsum[EX_NT / 64];
+__device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_t K, SelWs ws, uint32_t* h,
+                          uint32_t* scratch, uint32_t* wsum) {
     const int t = threadIdx.x;
     const int64_t C = nchunks(d);
-    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
-        if (!(ws.flags[row] & (F_OVERFLOW | F_SHORT))) continue;       // row-uniform
+    {
         const float* r = rows.row(row);
         uint32_t prefix = 0, krem = (uint32_t)K;
         for (int p = 0; p < 3; ++p) {
@@ -1001,6 +1011,17 @@ __global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t 
             ws.flags[row] = F_EXACT;
         }
         __syncthreads();
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, int64_t K, SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t wsum[EX_NT / 64];
+    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
+        if (!(ws.flags[row] & (F_OVERFLOW | F_SHORT))) continue;       // row-uniform
+        exact_row<VEC>(rows, n, row, d, K, ws, h, scratch, wsum);
     }
 }
 
@@ -1862,6 +1883,38 @@ __global__ __launch_bounds__(256) void k_assign_scatter(SelWs ws, float* __restr
     }
 }
 
+// A lone compressVector row on the fast path (its output zeroed by the filter): the exact fallback and
+// the scatter in ONE launch.  A failed row (overflow / short list / ambiguous ties) is selected
+// exactly by workgroup 0, which then scatters the rewritten list alone; otherwise every workgroup
+// scatters its shards as k_assign_scatter does.
+template <bool VEC>
+__global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d, int64_t K, SelWs ws, float* __restrict__ out) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t wsum[EX_NT / 64];
+    if (ws.flags[0] & (F_OVERFLOW | F_SHORT)) {                          // uniform over the grid
+        if (blockIdx.x != 0) return;
+        exact_row<VEC>(rows, 1, 0, d, K, ws, h, scratch, wsum);
+        __threadfence_block();
+        const uint32_t cnt = ws.rowcnt[0];
+        for (uint32_t e = threadIdx.x; e < cnt; e += EX_NT) out[ws.ent_idx[e]] = ws.ent_val[e];
+        return;
+    }
+    const uint32_t T = ws.thr[0], f = ws.flags[0];
+    const uint32_t cut = (f & F_TIES) ? ws.tiecut[0] : 0xFFFFFFFFu;
+    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
+    for (int sh = (int)blockIdx.x; sh < CS_SH; sh += (int)gridDim.x) {
+        const uint32_t cnt = ws.shcnt[sh * RCS];
+        const int64_t o = sh * segcap;
+        for (uint32_t e = threadIdx.x; e < cnt; e += EX_NT) {
+            const uint32_t ix = ws.ent_idx[o + e];
+            const float v = ws.ent_val[o + e];
+            const uint32_t key = mag_key(v);
+            if (key > T || (key == T && ix <= cut)) out[ix] = v;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Host orchestration
 // ------------------------------------------------------------------------------------------
@@ -1956,7 +2009,7 @@ static int filter_group() {
 
 template <int FGS>
 static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, SelWs ws, hipStream_t st,
-                          int shards) {
+                          int shards, float* zout = nullptr) {
     // oversubscribed grid (measured: 16-32 K blocks beat a resident-only persistent grid by ~5 %,
     // the hardware dispatcher balances the tail)
     const int64_t waves = rn * ((nchunks(d) + FGS - 1) / FGS);
@@ -1966,8 +2019,12 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
         const char* e = tuning_env("FLC_TK_RB");          // tuning runs only
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
-    hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
-                       std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards);
+    if (zout)
+        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, true>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
+                           std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
+    else
+        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
+                           std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, (float*)nullptr);
 }
 
 // Row groups of the TopK fast path whose candidate select + exact fallback run on a side stream
@@ -2118,6 +2175,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (ws_bytes < need) { set_error("select: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
     SelWs ws = carve_sel(wsp, codec, n, d, K, nullptr);
     const int64_t C = host_chunks(d);
+    bool lone_assign = false;
     // TopK, few rows: sharded candidate lists (k_topk_filter_fast) and the spread select (k_cs_pass)
     const bool few = codec == FLC_TOPK && n <= CS_FEW && !cs_single() && sel_capacity(codec, d, K) >= (int64_t)CS_SH * GCAP;
     if (codec == FLC_RANDK) {
@@ -2139,6 +2197,9 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         }
     } else {  // TOPK
         const bool dense_k = K * 16 > d;   // large K: the candidate list would not be smaller than the row
+        // a lone compressVector (assign, one row) on the fast path: output zeros from the filter, the
+        // exact fallback and the scatter in one launch (k_assign_finish)
+        lone_assign = assign && n == 1 && few && !dense_k && !assign_fold();
         if (dense_k) FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const int64_t bpr = (C + 3) / 4;
         if (!dense_k) {
@@ -2176,8 +2237,10 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 { ProfScope _ps("k_topk_filter", st);
                 // few rows: 2-chunk groups (twice the waves in flight for a lone row)
                 // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
-                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1);
-                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1); }
+                // a lone compressVector row: the filter also writes the dense output's zeros
+                float* zout = lone_assign ? out : nullptr;
+                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout);
+                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout); }
                 FLC_CHECK_LAUNCH("k_topk_filter");
                 if (TG > 1) {
                     FLC_CHECK_HIP(hipEventRecord(cx->ev[g], st));
@@ -2193,7 +2256,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 } else if (rn < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)rn), dim3(1024), 0, sside, r0, rn, K, ws);
                 else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(rn, 8192)), dim3(512), 0, sside, r0, rn, K, ws); }
                 FLC_CHECK_LAUNCH("k_cand_select");
-                {   // rows the fast path failed (rare): exact selection, one launch
+                if (!lone_assign) {   // rows the fast path failed (rare): exact selection, one launch
                     ProfScope _ps("k_topk_exact_rows", sside);
                     const int eb = grid_stride_blocks(rn, 2048);
                     if (vec) hipLaunchKernelGGL((k_topk_exact_rows<true>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, r0, rn, d, K, ws);
@@ -2233,6 +2296,14 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
+    if (lone_assign) {
+        // output zeros written by the filter; exact fallback (if the row failed) + scatter
+        ProfScope _ps("k_assign_finish", st);
+        if (vec) hipLaunchKernelGGL((k_assign_finish<true>), dim3(CS_SH), dim3(EX_NT), 0, st, rows, d, K, ws, out);
+        else hipLaunchKernelGGL((k_assign_finish<false>), dim3(CS_SH), dim3(EX_NT), 0, st, rows, d, K, ws, out);
+        FLC_CHECK_LAUNCH("k_assign_finish");
+        return FLC_OK;
+    }
     if (assign && n == 1 && codec == FLC_TOPK && !assign_fold()) {
         FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
         const int sb = (int)std::max<int64_t>(1, std::min<int64_t>((sel_capacity(codec, d, K) + 255) / 256, 2048));
