@@ -2253,7 +2253,10 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 if (few) {
                     for (int p = 0; p < 3; ++p)
                         hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws);
-                } else if (rn < 128) hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)rn), dim3(1024), 0, sside, r0, rn, K, ws);
+                } else if (rn < 128 || (TG > 1 && g == TG - 1))
+                    // few rows, or the last tail group (its select is exposed, nothing runs beside it):
+                    // 1024-thread workgroups, twice the loads in flight per row
+                    hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)rn), dim3(1024), 0, sside, r0, rn, K, ws);
                 else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(rn, 8192)), dim3(512), 0, sside, r0, rn, K, ws); }
                 FLC_CHECK_LAUNCH("k_cand_select");
                 if (!lone_assign) {   // rows the fast path failed (rare): exact selection, one launch
