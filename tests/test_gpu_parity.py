@@ -282,6 +282,31 @@ def test_topk_vs_oracle(ag, kind, n, d, k):
     assert_bitexact(one, enc[0])
 
 
+@pytest.mark.parametrize("kind", ["normal", "ties", "fewnz"])
+@pytest.mark.parametrize("n,d,k", [(256, 65548, 655), (130, 20011, 300)])
+def test_topk_tail_groups_vs_oracle(ag, kind, n, d, k):
+    """Many rows (n >= 128): the TopK uplink in tail row groups (4 groups at n = 256, 2 at 130) —
+    each group's candidate select and exact fallback on the side stream under the next group's
+    filter, the last group's select in 1024-thread workgroups, the fold split in two launches
+    (rows of the first groups beside the last select, tiles carried) — bit-exact vs the oracle,
+    with weights and through both entry points."""
+    g = np.random.default_rng([n, d, k, len(kind)])
+    rows = _topk_rows(kind, n, d, g)
+    enc = []
+    for i in range(n):
+        out = np.zeros(d, dtype=np.float32)
+        ind = oc.topk_indices(rows[i], k)
+        out[ind] = rows[i][ind]
+        enc.append(out)
+    w = [float(v) for v in g.uniform(0.5, 2.0, n)]
+    red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
+    rt = torch.from_numpy(rows).cuda()
+    assert_bitexact(red(rt), oc.reduce_plain(enc))
+    want_w = oc.reduce_plain(enc, w)
+    assert_bitexact(red(rt, weights=w), want_w)
+    assert_bitexact(red([rt[i] for i in range(n)], weights=w), want_w)
+
+
 def test_topk_c3_row_size(ag):
     """D = 10 M (the C3 row size), K = 1 %: bit-exact against the oracle's selection."""
     n, d = 2, 10_000_000
