@@ -4,7 +4,7 @@
 # Output under gpurun_out/ev_r03; copy what is judged into profiles/r03/.
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-out=gpurun_out/ev_r03
+out=gpurun_out/${EV_OUT:-ev_r03}
 mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
     --timeout-method thread -rf > $out/gpu_tests.log 2>&1 || exit $?
@@ -32,7 +32,7 @@ $B --dropin --workload c3 --n 8 --steps 10 --warmup 2 > $out/dropin_c3.log 2>&1 
 $B --dropin --workload c4 --n 4 --steps 5 --warmup 1 > $out/dropin_c4.log 2>&1 || exit $?
 $B --workload c3 --e2e --steps 5 --warmup 2 > $out/e2e_c3.log 2>&1 || exit $?
 # same-allocation A/B of this build against the previous one, if that build is present
-if [ -f flpytorch_amd/libflcodec_head.so ]; then
+if [ -f flpytorch_amd/libflcodec_head.so ]; then   # (optional: a previous build for a same-allocation check)
   timeout -k 10 400 python tools/ab_inproc.py --workload c3 --variants head,prod --rounds 3 > $out/inproc_c3.log 2>&1 || exit $?
   timeout -k 10 400 python tools/ab_inproc.py --workload c4 --variants head,prod --rounds 3 > $out/inproc_c4.log 2>&1 || exit $?
 fi
