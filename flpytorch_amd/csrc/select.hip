@@ -172,6 +172,9 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
             for (int u = 0; u < PU; ++u) keys[(p0 + u * GR + g0) * 256 + e] = mag_key(x[u]);
         }
     }
+    // a spread sample (S < d) only bounds the threshold: its keys to 22 bits (two passes, the low 9
+    // bits 0: a lower bound, ~6e-5 relative below the key); the whole row (S == d) exactly
+    const int NP = S == d ? 3 : 2;
     // rank (from the top) of the sample element whose key is the threshold
     uint32_t rank;
     if (S == d) {
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
     static_assert(!DUAL || NT >= 512, "hist_find2 takes 512 threads");
     auto rank_key = [&](uint32_t r) {
         uint32_t prefix = 0, krem = r;
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NP; ++p) {
             for (int i = threadIdx.x; i < HBINS; i += NT) h[i] = 0;
             __syncthreads();
             for (int i = threadIdx.x; i < S; i += NT) {
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
             krem -= above;
             __syncthreads();
         }
-        return prefix;
+        return NP == 3 ? prefix : prefix << 9;
     };
     auto rank_keys = [&](uint32_t ra, uint32_t rb, uint32_t& ka, uint32_t& kb) {
         if constexpr (!DUAL) {
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
             return;
         }
         uint32_t pa = 0, pb = 0, ma = ra, mb = rb;
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NP; ++p) {
             const bool same = pa == pb;
             for (int i = threadIdx.x; i < HBINS; i += NT) { h[i] = 0; h2[i] = 0; }
             __syncthreads();
@@ -227,8 +230,8 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
             pb = (pb << pass_bits(p)) | bb;
             mb -= ab;
         }
-        ka = pa;
-        kb = pb;
+        ka = NP == 3 ? pa : pa << 9;
+        kb = NP == 3 ? pb : pb << 9;
     };
     // the threshold key (rank), and the estimate of the K-th key (sample rank ks) that sizes the
     // first digit of k_cand_select
