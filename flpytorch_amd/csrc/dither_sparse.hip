@@ -64,7 +64,14 @@ constexpr int DS_NH = 2 * DS_FGS;          // fold tiles (half chunks) per item
 constexpr int DS_GCAP = 512;               // staged candidates per item (6.25 %; more -> row overflow)
 constexpr int DS_HCAP = DS_GCAP / DS_NH;    // entries per half chunk of an item (more -> row overflow)
 constexpr int DS_MAXLEV = 15;              // entry level field: 4 bits (a higher level -> row dense)
-constexpr int DS_SMAX = 16384;             // sample elements per row
+#ifndef FLC_DS_SMAX
+#define FLC_DS_SMAX 65536
+#endif
+#ifndef FLC_DS_MARGIN
+#define FLC_DS_MARGIN 0.02
+#endif
+constexpr int DS_SMAX = FLC_DS_SMAX;       // sample elements per row (256-element pieces)
+constexpr int DS_SNT = 1024;               // sample threads per row
 constexpr float DS_QT = 254.98f;
 constexpr int DS_MAXS = 512;               // level table entries kept in LDS by the fold
 constexpr uint32_t DS_OVF = 0xFFFFFFFFu;   // itm: the item overflowed its staging capacity
@@ -117,9 +124,10 @@ __device__ inline float f32_down(double v) { float f = (float)v; return (double)
 // ------------------------------------------------------------------------------------------
 // Sample: one workgroup per row.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64_t d, const float* __restrict__ levels,
-                                                   int s, uint64_t seed, int64_t client0, DsWs ws) {
-    __shared__ double r2[4], r4[4];
+__global__ __launch_bounds__(DS_SNT) void k_ds_sample(RowSrc rows, int64_t n, int64_t d, const float* __restrict__ levels,
+                                                      int s, uint64_t seed, int64_t client0, DsWs ws) {
+    constexpr int NW = DS_SNT / 64;
+    __shared__ double r2[NW], r4[NW];
     const int64_t row = blockIdx.x;
     if (blockIdx.x == 0) load_table(levels, s, ws.gtab);
     if (row >= n) return;
@@ -128,22 +136,24 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
     int64_t S;
     if (d <= DS_SMAX) {
         S = d;
-        for (int64_t i = threadIdx.x; i < d; i += 256) {
+        for (int64_t i = threadIdx.x; i < d; i += DS_SNT) {
             const double v = (double)r[i] * (double)r[i];
             a2 += v;
             a4 += v * v;
         }
     } else {
-        // 64 pieces of 256 contiguous elements spread evenly; thread t reads element t of 8 pieces
-        // per round trip
-        constexpr int P = DS_SMAX / 256;
+        // P pieces of 256 contiguous elements spread evenly; the block's 4 quarters take every 4th
+        // piece, thread t reading element t % 256 of 16 pieces per round trip
+        constexpr int P = DS_SMAX / 256, Q = DS_SNT / 256, U = 16;
+        static_assert(P % (Q * U) == 0, "sample pieces");
         S = DS_SMAX;
-        for (int p0 = 0; p0 < P; p0 += 8) {
-            float x[8];
+        const int e = threadIdx.x & 255, q = threadIdx.x >> 8;
+        for (int p0 = q; p0 < P; p0 += Q * U) {
+            float x[U];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) x[u] = r[((int64_t)(p0 + u) * (d - 256)) / (P - 1) + threadIdx.x];
+            for (int u = 0; u < U; ++u) x[u] = r[((int64_t)(p0 + Q * u) * (d - 256)) / (P - 1) + e];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const double v = (double)x[u] * (double)x[u];
                 a2 += v;
                 a4 += v * v;
@@ -155,8 +165,9 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
     if ((threadIdx.x & 63) == 0) { r2[threadIdx.x >> 6] = a2; r4[threadIdx.x >> 6] = a4; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        a2 = (r2[0] + r2[1]) + (r2[2] + r2[3]);
-        a4 = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+        a2 = 0.0;
+        a4 = 0.0;
+        for (int w = 0; w < NW; ++w) { a2 += r2[w]; a4 += r4[w]; }
         const float l0 = levels[0], l1 = levels[1];
         const bool bad = !(l0 == 0.f) || !(l1 > 0.f);   // the bounds need levels 0 < l1 < ...
         double nlo, nhi = __builtin_huge_val();
@@ -164,14 +175,14 @@ __global__ __launch_bounds__(256) void k_ds_sample(RowSrc rows, int64_t n, int64
             nlo = sqrt(a2) * (1.0 - 0x1p-20);              // the whole row: the norm itself
             nhi = sqrt(a2) * (1.0 + 0x1p-20);
         } else {
-            // estimate of the sum of squares, discounted by 6 sigma of the sample mean + 2 %; the
+            // estimate of the sum of squares, discounted by 6 sigma of the sample mean + a margin; the
             // upper bound only for light-tailed samples (heavy tails: n_hi unbounded, no sure entries)
             const double m = (double)S, mean2 = a2 / m;
             const double var = fmax(a4 / m - mean2 * mean2, 0.0);
             const double rel = sqrt(var / m) / mean2;      // NaN/inf when mean2 == 0 or overflow
-            const double f = fmin(fmax(1.0 - 6.0 * rel - 0.02, 0.25), 0.97);
+            const double f = fmin(fmax(1.0 - 6.0 * rel - FLC_DS_MARGIN, 0.25), 0.97);
             nlo = sqrt(f * mean2 * (double)d);
-            if (rel <= 0.05) nhi = sqrt((1.0 + 6.0 * rel + 0.02) * mean2 * (double)d);
+            if (rel <= 0.05) nhi = sqrt((1.0 + 6.0 * rel + FLC_DS_MARGIN) * mean2 * (double)d);
         }
         float nlof = (float)nlo;
         if (!(nlof >= 0.f) || !(nlof <= 3.0e38f)) nlof = 0.f;
@@ -1135,7 +1146,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     };
 
     { ProfScope _ps("k_ds_sample", st);
-    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(256), 0, st, rows, n, d, prm->d_levels, prm->s, prm->seed, client0, ws); }
+    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(DS_SNT), 0, st, rows, n, d, prm->d_levels, prm->s, prm->seed, client0, ws); }
     FLC_CHECK_LAUNCH("k_ds_sample");
     const int TO = tail_groups(n);
     if (K == 1 && TO <= 1) {

@@ -103,7 +103,7 @@ def test_sparse_dither_vs_oracle(ag, monkeypatch, kind, spec):
     assert_bitexact(got, want)
 
 
-@pytest.mark.parametrize("d", [1, 3, 4096, 4097, 8192 * 3 + 5, 16384, 16385, 100_000])
+@pytest.mark.parametrize("d", [1, 3, 4096, 4097, 8192 * 3 + 5, 16384, 16385, 65536, 65537, 100_000])
 def test_sparse_dither_shapes(ag, monkeypatch, d):
     """Chunk / item / sample boundaries, tiny rows (whole-row sample)."""
     n, client0 = 3, 0
