@@ -440,8 +440,13 @@ def dropin(args):
     if dither:
         for c in comps:                             # the uniforms on the device once (the protocol's lazy .to)
             c.testp = c.testp.to(dev)
+    # every client's row in turn (rows differ in their selection work, e.g. ties at the K-th key):
+    # the mean device time of one call
+    def all_rows():
+        for i in range(n):
+            comps[i].compressVector(rows[i])
     reps = max(args.steps, 20)
-    cv_ms = dev_time(lambda: comps[0].compressVector(rows[0]), reps)
+    cv_ms = dev_time(all_rows, max(reps // n, 3)) / n
     outs = [comps[i].compressVector(rows[i]) for i in range(n)]
     fold_ms = dev_time(lambda: ag.reduce_rows(x, outs, relative=False), max(args.steps, 5))
     cv_bytes = 8 * d + (8 * d if dither else 0)
@@ -464,15 +469,15 @@ def dropin(args):
             fn()
         torch.cuda.synchronize()
         res[name] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
-    # per-kernel device time of one compressVector (flc_profile scopes)
+    # per-kernel device time of one compressVector, over every client's row (flc_profile scopes)
     kernels = ["k_topk_sample", "k_topk_filter", "k_cand_select", "k_topk_exact_rows", "k_chunk_accum",
                "k_norm_partials", "k_ew_accum_vec", "k_ew_encode", "k_randk_scatter_dev", "k_assign_scatter",
                "k_assign_finish"]
     _lib.profile_enable(True)
     for k in kernels:
         _lib.profile_collect(k)
-    for _ in range(10):
-        comps[0].compressVector(rows[0])
+    for _ in range(max(10 // n, 2)):
+        all_rows()
     torch.cuda.synchronize()
     _lib.profile_enable(False)
     per_kernel = {}

@@ -381,7 +381,10 @@ __global__ __launch_bounds__(NT) void k_cand_select(int64_t r0, int64_t rn, int6
 // histogram (atomics); the last workgroup to arrive picks the digit (the same digits, bins and
 // results as k_cand_select) and leaves the row's state for the next launch — one launch per digit
 // instead of one latency-bound workgroup walking 1.4 K candidates twice.  Ambiguous ties at the
-// K-th key send the row to the exact path (k_topk_exact_rows: the same lowest-index rule).
+// K-th key (more entries equal to it than places left; ~1 row in 8 at D = 10 M) are resolved by the
+// last arriver as k_cand_select does: the tie indices gathered over all shards, the krem-th smallest
+// is the admission cut (the reference keeps the lowest indices).  Only more than TIECAP ties take
+// the exact path.
 // ------------------------------------------------------------------------------------------
 constexpr int CS_NT = 256;
 __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
@@ -461,17 +464,70 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
     __syncthreads();
     uint32_t bin, above;
     hist_find(h, krem, bin, above, scratch);
+    const uint32_t last = h[bin];
+    const uint32_t np = first ? bin : ((prefix << (sh - s1)) | bin);
+    const uint32_t nk = krem - above;
+    const bool clamp = first && bin == HBINS - 1;                        // K-th key in the clamp bin
+    bool ties = !clamp && s1 == 0u && last > nk, tie_fail = ties && last > TIECAP;
+    if (ties && !tie_fail) {
+        // gather the indices of the entries with key == thr over all shards (4 threads per shard,
+        // 8 float4 per thread in flight), then the nk-th smallest index is the cut
+        static_assert(CS_NT == 4 * CS_SH, "tie gather: 4 threads per shard");
+        __syncthreads();                                                 // h[bin] read by every thread
+        uint32_t* tix = h;
+        if (threadIdx.x == 0) scratch[0] = 0;
+        __syncthreads();
+        const uint32_t thr = T + np;
+        const int k = threadIdx.x >> 2;
+        const uint32_t sub = threadIdx.x & 3u, c = shc[k * RCS], c4 = c >> 2;
+        const float* sv = ws.ent_val + row * ws.cap + k * segcap;
+        const uint32_t* si = ws.ent_idx + row * ws.cap + k * segcap;
+        const float4* s4 = reinterpret_cast<const float4*>(sv);
+        auto test = [&](float x, uint32_t pos) {
+            if (mag_key(x) == thr) {
+                const uint32_t slot = atomicAdd(&scratch[0], 1u);
+                if (slot < TIECAP) tix[slot] = si[pos];
+            }
+        };
+        uint32_t j = sub;
+        for (; j + 28u < c4; j += 32u) {
+            float4 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) q[u] = cs_ld(s4 + j + 4u * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t p4 = (j + 4u * u) * 4u;
+                test(q[u].x, p4); test(q[u].y, p4 + 1u); test(q[u].z, p4 + 2u); test(q[u].w, p4 + 3u);
+            }
+        }
+        for (; j < c4; j += 4u) {
+            const float4 q = cs_ld(s4 + j);
+            test(q.x, j * 4u); test(q.y, j * 4u + 1u); test(q.z, j * 4u + 2u); test(q.w, j * 4u + 3u);
+        }
+        for (uint32_t t = c4 * 4u + sub; t < c; t += 4u) test(sv[t], t);
+        __syncthreads();
+        const uint32_t m = scratch[0];                                   // == last
+        if (m != last) tie_fail = true;                                  // (uniform: scratch[0] in LDS)
+        else
+            for (uint32_t a = threadIdx.x; a < m; a += CS_NT) {
+                const uint32_t ia = tix[a];
+                uint32_t rank = 0;
+                for (uint32_t bb = 0; bb < m; ++bb) rank += tix[bb] < ia ? 1u : 0u;
+                if (rank == nk - 1u) ws.tiecut[row] = ia;                // indices are distinct
+            }
+    }
     if (threadIdx.x == 0) {
         atomicExch(&ws.carrive[row * RCS], 0u);
-        const uint32_t last = h[bin];
-        const uint32_t np = first ? bin : ((prefix << (sh - s1)) | bin);
-        const uint32_t nk = krem - above;
-        if (first && bin == HBINS - 1) {                                 // K-th key in the clamp bin
+        if (clamp) {
             ws.flags[row] |= F_SHORT;
             cs[3] = 2u;
         } else if (s1 == 0u) {
-            if (last > nk) ws.flags[row] |= F_SHORT;                     // ambiguous ties: exact path
-            else { ws.thr[row] = T + np; ws.krem[row] = nk; }
+            if (tie_fail) ws.flags[row] |= F_SHORT;                      // > TIECAP ties: exact path
+            else {
+                ws.thr[row] = T + np;
+                ws.krem[row] = nk;
+                if (ties) ws.flags[row] |= F_TIES;
+            }
             cs[3] = 2u;
         } else {
             cs[0] = s1; cs[1] = np; cs[2] = nk; cs[3] = 1u;
@@ -665,7 +721,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
         ring[L] = load_q(rs, lane, L);
         __builtin_amdgcn_sched_barrier(0);   // issue in ring order: the loop's static vmcnt waits assume it
     }
-    // few rows (shards > 1): item t reserves in shard t % shards of its row's list (a counter and a
+    // few rows (shards > 1): group g of a row reserves in shard g % shards of its list (a counter and a
     // region of its own): one counter per row would serialise the reservation atomics of every
     // wave on one address (~90 per microsecond), a lone 10 M row's ~1.2 K of them took longer than
     // its loads
@@ -781,7 +837,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
         }
         if (pv) finish(par ^ 1);
         uint32_t res = 0;
-        const int64_t shard = shards > 1 ? it % shards : 0;
+        // the shard of the group's index within its row (the item order interleaves rows: `it % shards`
+        // put each of n rows' items into only 64 / n shards, which overflowed them)
+        const int64_t shard = shards > 1 ? (cg0 / FGS) % shards : 0;
         if (cnt && cnt <= GCAP && lane == 0)
             res = atomicAdd(shards > 1 ? &ws.shcnt[(row * shards + shard) * RCS] : &ws.rowcnt[(row) * RCS], cnt);
         pv = true; prow = row; pc0 = cg0; pcc = ccp; ptot = cnt; pres = res; pseg = shard;

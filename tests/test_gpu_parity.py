@@ -307,6 +307,68 @@ def test_topk_tail_groups_vs_oracle(ag, kind, n, d, k):
     assert_bitexact(red([rt[i] for i in range(n)], weights=w), want_w)
 
 
+@pytest.mark.parametrize("d", [2_000_000, 10_000_000])
+def test_topk_few_rows_kth_ties_vs_oracle(ag, d):
+    """Few rows (the sharded lists + k_cs_pass path of a lone compressVector and of n <= 16 uplinks)
+    whose K-th magnitude is tied by entries in different shards, with fewer places left than ties:
+    the last arriver gathers the tie indices and admits the lowest (torch.topk's CPU order, the
+    oracle's), instead of the exact path.  Bit-exact for the fused uplink (weighted too) and for
+    compressVector of each row."""
+    n, k = 3, d // 100
+    g = np.random.default_rng([d, 7])
+    rows = g.standard_normal((n, d)).astype(np.float32)
+    for i, top in enumerate([0, 2, 5]):                  # ties straddle: 1, 3, 6 places left
+        mags = np.sort(np.abs(rows[i]))[::-1]
+        v = mags[k - 1 - top]
+        below = np.flatnonzero(np.abs(rows[i]) < mags[k + 10])
+        pos = below[np.linspace(0, len(below) - 1, 6 + i).astype(np.int64)]
+        rows[i, pos] = v * np.where(g.random(len(pos)) < 0.5, -1.0, 1.0).astype(np.float32)
+    enc = []
+    for i in range(n):
+        out = np.zeros(d, dtype=np.float32)
+        ind = oc.topk_indices(rows[i], k)
+        out[ind] = rows[i][ind]
+        enc.append(out)
+    red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
+    rt = torch.from_numpy(rows).cuda()
+    assert_bitexact(red(rt), oc.reduce_plain(enc))
+    w = [0.75, 1.5, 1.0]
+    assert_bitexact(red(rt, weights=w), oc.reduce_plain(enc, w))
+    c = ag.initCompressor(f"topk:{k}", d)
+    for i in range(n):
+        assert_bitexact(c.compressVector(rt[i]), enc[i])
+
+
+def test_topk_few_rows_stay_on_fast_path(ag):
+    """Performance guard for the few-row path (n <= 16: sharded lists + k_cs_pass): Gaussian rows at
+    D = 10 M must not fall back to the exact selection (~8 ms per failed row against ~0.1 ms).  Two
+    round-3 builds did: the fused uplink's interleaved item order put each of n rows' groups into
+    64 / n shards (overflow), and ambiguous ties at the K-th key (~1 row in 8) went to the exact path."""
+    n, d = 8, 10_000_000
+    k = d // 100
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    rows = torch.randn(n, d, generator=gen, device="cuda")
+    red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
+    c = ag.initCompressor(f"topk:{k}", d)
+
+    def dev_ms(fn, reps=3):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    fused = dev_ms(lambda: red(rows))
+    assert fused < 3.0, f"fused {n}-row uplink {fused:.2f} ms: a row took the exact path"
+    for i in range(n):
+        one = dev_ms(lambda: c.compressVector(rows[i]))
+        assert one < 2.0, f"compressVector of row {i}: {one:.2f} ms: the exact path"
+
+
 def test_topk_c3_row_size(ag):
     """D = 10 M (the C3 row size), K = 1 %: bit-exact against the oracle's selection."""
     n, d = 2, 10_000_000
