@@ -502,6 +502,45 @@ def dropin(args):
                               "and uploads it; the second line reuses the drawn patterns"}))
 
 
+def launch_ranks(gpus, cmd, poll_s=0.2, grace_s=10.0):
+    """One process per GPU without an outside launcher (`python3 bench.py --gpus G`): G fresh
+    children of ``cmd``, each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in its
+    environment (torch.distributed.run's contract, rendezvous on 127.0.0.1), started before this
+    process has made any GPU call — the parent never re-execs itself and never touches the GPU.
+    Waits for every rank; when one fails the others are terminated (then killed after grace_s) so
+    a rank stuck in a collective cannot hang the job.  Returns 0, or the first failing rank's exit
+    status (a signal as 128 + signo).  Replaces the reference's thread-per-device dispatch
+    (thread_pool.py:56-67) with one process per GPU."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+    status, failed_at = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        for c in codes:
+            if c is not None and c != 0 and status == 0:
+                status = c if c > 0 else 128 - c
+                failed_at = time.monotonic()
+                for p in procs:
+                    if p.poll() is None:
+                        p.send_signal(signal.SIGTERM)
+        if all(c is not None for c in codes):
+            return status
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(poll_s)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -545,6 +584,10 @@ def main():
         return e2e(args)
     if args.wire:
         return wire(args)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no outside launcher: this process starts the G ranks itself (nothing has touched the GPU yet)
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
 
     wl = dict(WORKLOADS[args.workload])
     if args.n:

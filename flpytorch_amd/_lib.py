@@ -9,10 +9,11 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# FLC_LIB_VARIANT=<tag> loads flpytorch_amd/libflcodec_<tag>.so instead (A/B tuning runs of two
-# builds in one process tree on one box; tools/ab_build.sh makes them).
-LIB_PATH = os.path.join(_HERE, "libflcodec%s.so" % (
-    ("_" + os.environ["FLC_LIB_VARIANT"]) if os.environ.get("FLC_LIB_VARIANT") else ""))
+# A/B variant builds (tools/ab_build.sh) live in <repo>/abvar/libflcodec_<tag>.so, outside the
+# package: FLC_LIB_VARIANT=<tag> loads one instead of the product library (tuning runs only).
+VARIANT_DIR = os.path.join(os.path.dirname(_HERE), "abvar")
+LIB_PATH = (os.path.join(VARIANT_DIR, "libflcodec_%s.so" % os.environ["FLC_LIB_VARIANT"])
+            if os.environ.get("FLC_LIB_VARIANT") else os.path.join(_HERE, "libflcodec.so"))
 
 FLC_OK, FLC_ERR_ARG, FLC_ERR_DTYPE, FLC_ERR_HIP, FLC_ERR_WORKSPACE, FLC_ERR_UNSUPPORTED = range(6)
 FLC_IDENT, FLC_LAZY, FLC_RANDK, FLC_NATURAL, FLC_STD_DITHERING, FLC_NAT_DITHERING, FLC_TOPK, FLC_RANK_K = range(1, 9)
@@ -39,7 +40,7 @@ EXPORTS = [
     "flc_mt_choice", "flc_mt_rand", "flc_mt_randint31",
     "flc_device_uniform", "flc_device_randk_indices",
     "flc_device_randk_counts_workspace_size", "flc_device_randk_counts",
-    "flc_profile_enable", "flc_profile_collect",
+    "flc_profile_enable", "flc_profile_collect", "flc_select_row_flags",
     "flc_selftest_division",
 ]
 
@@ -96,9 +97,10 @@ def load():
 
 def open_variant(tag):
     """Another build of the library for an in-process A/B (tools/ab_inproc.py): tag "" or "prod" is
-    the product libflcodec.so, else flpytorch_amd/libflcodec_<tag>.so.  Not cached; make it the one
+    the product libflcodec.so, else abvar/libflcodec_<tag>.so.  Not cached; make it the one
     every wrapper calls with ``use(lib)``."""
-    path = os.path.join(_HERE, "libflcodec.so" if tag in ("", "prod") else f"libflcodec_{tag}.so")
+    path = (os.path.join(_HERE, "libflcodec.so") if tag in ("", "prod")
+            else os.path.join(VARIANT_DIR, f"libflcodec_{tag}.so"))
     if not os.path.exists(path):
         raise ImportError(f"flpytorch_amd: {path} is missing")
     return _bind(ctypes.CDLL(path))
@@ -171,7 +173,11 @@ def _bind(lib):
     lib.flc_profile_enable.argtypes = [i32]
     lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
     lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
+    if hasattr(lib, "flc_select_row_flags"):        # (absent from A/B builds of older revisions)
+        lib.flc_select_row_flags.argtypes = [P(FlcCodecParams), i64, i64, vp, sz, vp, vp]
     for name in EXPORTS:
+        if not hasattr(lib, name):
+            continue
         if name not in ("flc_version", "flc_build_id", "flc_last_error_string", "flc_device_uniform",
                         "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
                         "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",

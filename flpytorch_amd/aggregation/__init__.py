@@ -7,7 +7,7 @@ classes whose reduction is the shared sequential fold (algorithms.py:1753-1768),
 """
 from .compressors import (Compressor, CompressorType, initCompressor, stream_choice, stream_rand,  # noqa: F401
                           stream_random, stream_randint31)
-from .fused import PayloadReducer, UplinkReducer  # noqa: F401
+from .fused import PayloadReducer, UplinkReducer, select_row_flags  # noqa: F401
 from .mixed import MixedUplink  # noqa: F401
 from .shift import dianaStep, ef21Step, marinaStep  # noqa: F401
 from .reduce import (make_server_gradient_frecon, reduce_client_models, reduce_rows,  # noqa: F401

@@ -22,13 +22,40 @@ from .. import _lib
 from .compressors import Compressor, CompressorType
 
 
+def _device(device):
+    """torch.device with its index resolved (``'cuda'`` -> the current device), so that it compares
+    equal to a stream's device."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def select_row_flags(comp: Compressor, n, d, device=None):
+    """Path report of the last TopK call on this thread's workspace (flc_select_row_flags): a
+    [n] int64 tensor of row state bits — 1 overflow, 2 short list, 4 ties cut on the fast path,
+    8 exact path.  Call it right after the UplinkReducer / compressVector call, with its n and d
+    (compressVector: n = 1).  Tests use it to assert which path ran."""
+    dev = _device(device)
+    lib = _lib.load()
+    prm, _ = comp.codec_params(dev)
+    ws_bytes = lib.flc_encode_reduce_workspace_size(ctypes.byref(prm), n, d)
+    ws = _lib.WORKSPACE.get(dev, ws_bytes)
+    flags = torch.zeros(n, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.flc_select_row_flags(ctypes.byref(prm), n, d, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                      ctypes.c_void_p(flags.data_ptr()), _lib.stream_ptr(dev))
+    _lib.check(rc, "flc_select_row_flags")
+    return flags.cpu().to(torch.int64)
+
+
 class UplinkReducer:
     """Holds the codec constants + workspace for repeated fused encode+reduce calls."""
 
     def __init__(self, compressor: Compressor, device=None, seed=None):
         _lib.require_gpu()
         self.comp = compressor
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = _device(device)
         self.seed = seed
 
     def params(self):
@@ -157,7 +184,7 @@ class PayloadReducer:
     def __init__(self, compressor: Compressor, device=None):
         _lib.require_gpu()
         self.comp = compressor
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = _device(device)
 
     def __call__(self, payloads, d=None, out=None, weights=None, divisor=None):
         """payloads: [N, ld] uint8 device tensor (rows 16-byte aligned, ld % 16 == 0) or a list of

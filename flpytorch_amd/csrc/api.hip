@@ -103,6 +103,12 @@ extern "C" int flc_profile_collect(const char* kernel, double* h_total_ms, int64
 
 extern "C" const char* flc_last_error_string(void) { return g_err; }
 
+extern "C" int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* d_workspace,
+                                    size_t ws_bytes, uint32_t* d_flags, void* stream) {
+    if (!prm || (n > 0 && (!d_workspace || !d_flags))) { set_error("flc_select_row_flags: null argument"); return FLC_ERR_ARG; }
+    return sel_row_flags(prm, n, d, d_workspace, ws_bytes, d_flags, (hipStream_t)stream);
+}
+
 namespace flc {
 int selftest_division(const float* d_b, int nb, unsigned long long* d_bad, hipStream_t st);
 }

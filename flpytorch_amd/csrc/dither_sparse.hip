@@ -84,6 +84,15 @@ constexpr int DS_AP = FLC_DS_AP;           // rows of entry lists in flight in t
 // that alias (C5's replayed pool) are still read from HBM once per client
 constexpr int64_t DS_RB = 16;
 constexpr int DS_RINGC = 4;                // compat filter ring (x + u: 24 B per lane per step)
+// Per-lane candidate staging (device-RNG filter): each lane appends its candidates to its own
+// column of the wave's staging, slot row min(count, DS_PLS) (row DS_PLS absorbs a lane's
+// overflow), so the per-element path has no cross-lane prefix (ballot / mbcnt) and no scalar
+// counter chain; the columns are compacted once per item.  A lane with more than DS_PLS
+// candidates in an item (Poisson(2.7) at C4: ~4e-3 of items) re-reads its elements afterwards.
+#ifndef FLC_DS_PL
+#define FLC_DS_PL 0
+#endif
+constexpr int DS_PLS = 10;
 
 // One entry of the fold's lists (u16): half-chunk-local index (11 bits) | sign << 11 | level << 12;
 // its contribution is copysign(levels[level], sign) * norm — C(x) exactly as the encode forms it.
@@ -260,8 +269,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
     constexpr int DS_ITEM_STORES = 4 + GCAP / 128;   // partial, itm, tab, sure and ambiguous copy-outs
     // (entry word, x bits); 64 slots past GCAP take the writes of a wave-instruction that starts
     // at GCAP (its item has overflowed)
-    __shared__ uint2 stage[4][GCAP + 64];
-    __shared__ __attribute__((aligned(16))) uint16_t stage16[4][GCAP];
+    // per-lane staging (PL): DS_PLS + 1 slot rows of 64 lanes, compacted in place into the item's
+    // list; its sure entries (4 halves x DS_HCAP u16 = 1 KB) then go to entries [GCAP, GCAP + 128)
+    constexpr bool PL = FLC_DS_PL && !COMPAT && PROBE == 0;
+    constexpr int SROWS = PL ? (DS_PLS + 1) * 64 : GCAP + 64;
+    static_assert(!PL || (SROWS >= GCAP + 128 && DS_PLS * 64 >= GCAP / 2), "per-lane staging layout");
+    __shared__ __attribute__((aligned(16))) uint2 stage[4][SROWS];
+    __shared__ __attribute__((aligned(16))) uint16_t stage16[4][PL ? 8 : GCAP];
     __shared__ float stagef[4][COMPAT ? GCAP + 64 : 1];     // compat: RD(u) of the staged
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -272,7 +286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
     if (it >= items) return;
     const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
     uint2* sg = stage[wv];
-    uint16_t* s16 = stage16[wv];
+    uint16_t* s16 = PL ? reinterpret_cast<uint16_t*>(stage[wv] + GCAP) : stage16[wv];
     float* sgf = stagef[wv];
     // LDS byte address of the wave's staging buffer (wave-uniform)
     const uint32_t sla = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint2*)sg);
@@ -315,6 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
         const int64_t gi = c / FGS;
         const int64_t nit = it + stride;
         uint32_t cnt = 0;
+        uint32_t lcnt = 0;                                   // PL: this lane's candidates in the item
         double a2 = 0.0;
         int64_t nrow = row, nc = c;
 #pragma unroll
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
                         // no range test: past the row end the loads return 0, and a zero candidate
                         // is dropped; NaN from 0 * inf (qc = inf) is not a candidate
                         const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
-                        const uint64_t m = __ballot(f);
+                        const uint64_t m = PL ? 0ull : __ballot(f);
                         // exec-masked store (a branch-free store of every element to a per-lane spill
                         // slot measured 9.2 -> 11.9 ms: the staging is LDS-issue sensitive)
                         if (PROBE == 5) {
@@ -401,6 +416,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
                                          "ds_write2_b32 %2, %3, %4 offset1:1\n\ts_mov_b64 exec, %0"
                                          : "=&s"(saved) : "s"(m), "v"(la), "v"(jb + (uint32_t)(L * 256 + q)), "v"(__float_as_uint(vq[q]))
                                          : "memory");
+                        } else if (PL) {
+                            // the lane's own column: slot row min(lcnt, DS_PLS), 512 B per row
+                            const uint32_t la = sla + (uint32_t)lane * 8u + min(lcnt, (uint32_t)DS_PLS) * 512u;
+                            if (f)
+                                asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(jb + (uint32_t)(L * 256 + q)),
+                                             "v"(__float_as_uint(vq[q])) : "memory");
+                            lcnt += f ? 1u : 0u;
+                            continue;
                         } else if (PROBE != 2 && f) {
 #if FLC_DS_W2
                             // slot = min(cnt, GCAP) + candidates in lower lanes (< GCAP + 64): exact
@@ -432,6 +455,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
             ru = run;
         }
         a2 = wave_sum(a2);                                   // fixed butterfly: deterministic
+        if constexpr (PL) {
+            // Compaction in place: slot row k of every lane with more than k candidates, in row
+            // order, lanes in order within a row.  An entry's new position never exceeds its slot
+            // (k * 64 + lane) and a row is read before any of it is written, so nothing unread is
+            // overwritten.  (The list order is free: k_ds_resolve / k_ds_accum do not depend on it.)
+            const uint32_t lc = min(lcnt, (uint32_t)DS_PLS);
+            for (uint32_t k = 0; k < (uint32_t)DS_PLS; ++k) {
+                const bool v = k < lc;
+                const uint64_t mk = __ballot(v);
+                if (mk == 0) break;
+                if (v) {
+                    const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                    const uint2 e = sg[k * 64 + lane];
+                    sg[pos] = e;
+                }
+                cnt += (uint32_t)__popcll(mk);
+            }
+            // Lanes past DS_PLS (rare): their candidates from #DS_PLS on were absorbed by the last
+            // row; re-read those lanes' elements of the item and append them (the loads wait
+            // behind the ring's, once)
+            const bool ovl = lcnt > (uint32_t)DS_PLS;
+            if (__ballot(ovl)) {
+                if (cnt + 0u <= (uint32_t)GCAP) {
+                    // one element per step, nothing unrolled: the ring (the next item's loads in
+                    // flight) stays live in registers across this path
+                    const int64_t cg = gi * FGS;
+                    uint32_t seen = 0;
+#pragma unroll 1
+                    for (int e = 0; e < FGS * 64; ++e) {
+                        const int sub = e >> 6, L = (e >> 2) & 15, q = e & 3;
+                        const auto rso = chunk_rsrc(rows.row_s(row), (cg + sub) * CHUNK, d);
+                        const float x = ovl ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rso, lane * 16 + q * 4, L * 1024, 0)) : 0.f;
+                        const uint32_t hg = gmix(lphi + (uint32_t)((cg + sub) * 1024 + L * 64) * 0x9E3779B1u + rk);
+                        const float hi = (float)((hg >> (8 * q)) & 0xFFu);
+                        const bool f = ovl && fmaf(fabsf(x), qc, hi) > DS_QT;
+                        const bool extra = f && seen >= (uint32_t)DS_PLS;
+                        seen += f ? 1u : 0u;
+                        const uint64_t me = __ballot(extra);
+                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(me >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)me, 0u));
+                        if (extra && pos < (uint32_t)GCAP + 64u)
+                            sg[pos] = make_uint2((uint32_t)(sub * CHUNK + L * 256 + q) + (uint32_t)lane * 4u, __float_as_uint(x));
+                        cnt += (uint32_t)__popcll(me);
+                    }
+                } else {
+                    cnt = GCAP + 1;                          // the item overflows anyway
+                }
+            }
+        }
         const bool fits = cnt <= GCAP;
         const uint32_t base = (uint32_t)gi * GCAP;
         // Classification of the staged candidates (LDS and ALU only: no vector-memory op between

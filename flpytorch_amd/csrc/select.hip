@@ -2080,6 +2080,7 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
         const char* e = tuning_env("FLC_TK_RB");          // tuning runs only
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
+    ProfScope _pv(FGS == 4 ? "k_topk_filter_g4" : "k_topk_filter_g2", st);   // which variant ran (tests)
     if (zout)
         hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, true>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
@@ -2376,6 +2377,19 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
         return FLC_OK;
     }
     return launch_chunk_accum(n, d, ws, assign, w, wt, out, st);
+}
+
+// flc_select_row_flags: the rows' state words the last TopK sel_run left in the workspace
+int sel_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* wsp, size_t ws_bytes,
+                  uint32_t* flags, hipStream_t st) {
+    if (prm->codec != FLC_TOPK) { set_error("flc_select_row_flags: TopK only"); return FLC_ERR_ARG; }
+    if (n <= 0 || d <= 0) return FLC_OK;
+    size_t need = 0;
+    carve_sel(nullptr, prm->codec, n, d, prm->k, &need);
+    if (ws_bytes < need) { set_error("flc_select_row_flags: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
+    const SelWs ws = carve_sel(const_cast<void*>(wsp), prm->codec, n, d, prm->k, nullptr);
+    FLC_CHECK_HIP(hipMemcpyAsync(flags, ws.flags, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    return FLC_OK;
 }
 
 // ------------------------------------------------------------------------------------------

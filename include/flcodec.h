@@ -291,10 +291,22 @@ int flc_selftest_division(const float* d_divisors, int n, unsigned long long* d_
  * bracketed by hipEvents recorded on the launch stream; flc_profile_collect() waits for them
  * and returns the summed duration and launch count for one kernel name, then forgets them.
  * Names: k_topk_filter, k_topk_sample, k_radix_hist, k_chunk_accum, k_ew_accum_vec,
- * k_norm_partials, k_reduce_vec, k_randk_scatter.
+ * k_norm_partials, k_reduce_vec, k_randk_scatter; the TopK filter's variant is recorded too
+ * (k_topk_filter_g4: 4-chunk work items, the many-row path of large launches; k_topk_filter_g2:
+ * 2-chunk items), so a test can assert which one ran.
  * -------------------------------------------------------------------------------------- */
 int flc_profile_enable(int on);
 int flc_profile_collect(const char* kernel, double* h_total_ms, int64_t* h_launches);
+
+/* Path report of the last TopK selection (test hook, no compute): copies the per-row state
+ * words the previous flc_encode_reduce / flc_encode (TopK) left in d_workspace — called with the
+ * same params, n and d — into d_flags[n] (device, on `stream`).  Bits: 1 the candidate list
+ * overflowed, 2 it came up short, 4 ambiguous ties at the K-th key resolved on the fast path,
+ * 8 the row was selected by the exact path (the fast path failed, or K > D/16).  Rows that stayed
+ * on the fast path read 0 or 4.  (Replaces nothing in the reference: compressors.py:330-335 has
+ * one path.) */
+int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* d_workspace,
+                         size_t ws_bytes, uint32_t* d_flags, void* stream);
 
 #ifdef __cplusplus
 }

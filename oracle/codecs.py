@@ -240,10 +240,26 @@ def topk_keys(x):
 
 
 def topk_indices(x, K):
-    """Indices of the K largest |x|, ties at the K-th magnitude broken by lowest index."""
+    """Indices of the K largest |x|, ties at the K-th magnitude broken by lowest index
+    (compressors.py:330-335 with torch.topk's CPU tie order)."""
     key = topk_keys(x).astype(np.int64)
     order = np.lexsort((np.arange(key.size), -key))
     return np.sort(order[:K])
+
+
+def topk_indices_fast(x, K):
+    """topk_indices by selection instead of a full sort (same set; large rows in the GPU tests):
+    every key above the K-th key, then the lowest-index keys equal to it."""
+    key = topk_keys(x)
+    K = int(K)
+    if K <= 0:
+        return np.empty(0, dtype=np.int64)
+    if K >= key.size:
+        return np.arange(key.size, dtype=np.int64)
+    kth = np.partition(key, key.size - K)[key.size - K]
+    above = np.flatnonzero(key > kth)
+    ties = np.flatnonzero(key == kth)[:K - above.size]
+    return np.sort(np.concatenate([above, ties])).astype(np.int64)
 
 
 def server_gradient(x, models, weights=None):

@@ -1,0 +1,61 @@
+"""bench.py's own rank launcher (`python3 bench.py --gpus G` without torchrun), on CPU.
+
+launch_ranks() starts G children with torch.distributed.run's environment contract and propagates
+their exit status; a failed rank must take the others down instead of leaving them waiting in a
+collective.  The GPU end-to-end run is tests/test_gpu_dist.py::test_bench_self_launch_*.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_ranks_get_the_rendezvous_environment(tmp_path):
+    out = tmp_path / "env"
+    code = ("import os, json; k = ['RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT'];"
+            f"open(r'{out}' + os.environ['RANK'], 'w').write(json.dumps({{x: os.environ[x] for x in k}}))")
+    assert bench.launch_ranks(3, [sys.executable, "-c", code]) == 0
+    envs = [json.loads((tmp_path / f"env{r}").read_text()) for r in range(3)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"3"} and {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+
+
+def test_failed_rank_ends_the_job():
+    code = "import os, sys, time; r = int(os.environ['RANK']); sys.exit(3) if r == 1 else time.sleep(120)"
+    t0 = time.monotonic()
+    assert bench.launch_ranks(2, [sys.executable, "-c", code], grace_s=5.0) == 3
+    assert time.monotonic() - t0 < 30
+
+
+def test_killed_rank_reports_its_signal():
+    code = "import os, signal; r = int(os.environ['RANK']); os.kill(os.getpid(), signal.SIGKILL) if r == 0 else None"
+    assert bench.launch_ranks(2, [sys.executable, "-c", code]) == 128 + 9
+
+
+def test_ranks_rendezvous_over_gloo():
+    code = ("import torch, torch.distributed as dist; dist.init_process_group('gloo');"
+            "t = torch.ones(4) * (dist.get_rank() + 1); dist.all_reduce(t);"
+            "assert t.tolist() == [3.0] * 4, t; dist.destroy_process_group()")
+    assert bench.launch_ranks(2, [sys.executable, "-c", code]) == 0
+
+
+@pytest.mark.timeout(180)
+def test_bench_without_gpu_fails_loudly_not_hangs():
+    """The real entry point through the launcher on a host without a GPU: every rank fails at its
+    first device call, the parent returns non-zero and prints no result line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FLC_BENCH_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--no-cpu-baseline"], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=170)
+    if p.returncode == 0:
+        pytest.skip("a GPU is visible here")
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]

@@ -258,7 +258,41 @@ def _topk_rows(kind, n, d, g):
         r[:, 5] = np.inf
         r[:, 11] = -np.inf
         return r
+    if kind == "heavy":              # SURVEY 8d's second distribution: N(0,1) * 10^U(-3,3)
+        r = g.standard_normal((n, d), dtype=np.float32)
+        r *= np.float32(10.0) ** g.uniform(-3, 3, (n, d)).astype(np.float32)
+        return r
     raise ValueError(kind)
+
+
+def _topk_enc(rows, k):
+    """The oracle's dense TopK outputs (compressors.py:330-335, lowest-index ties)."""
+    enc = []
+    for r in rows:
+        out = np.zeros(r.size, dtype=np.float32)
+        ind = oc.topk_indices_fast(r, k)
+        out[ind] = r[ind]
+        enc.append(out)
+    return enc
+
+
+class _FilterVariants:
+    """Counts the TopK filter launches by variant (flc_profile_*: k_topk_filter_g4 / _g2) over a block."""
+
+    def __enter__(self):
+        from flpytorch_amd import _lib
+        self._lib = _lib
+        _lib.profile_enable(True)
+        for v in ("k_topk_filter_g4", "k_topk_filter_g2"):
+            _lib.profile_collect(v)
+        return self
+
+    def __exit__(self, *exc):
+        torch.cuda.synchronize()
+        self.g4 = self._lib.profile_collect("k_topk_filter_g4")[1]
+        self.g2 = self._lib.profile_collect("k_topk_filter_g2")[1]
+        self._lib.profile_enable(False)
+        return False
 
 
 @pytest.mark.parametrize("kind", ["normal", "ties", "zeros", "clustered", "nan_inf", "fewnz"])
@@ -332,18 +366,26 @@ def test_topk_few_rows_kth_ties_vs_oracle(ag, d):
     red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
     rt = torch.from_numpy(rows).cuda()
     assert_bitexact(red(rt), oc.reduce_plain(enc))
+    # the tie cut ran on the fast path (F_TIES, 4) and no row fell back to the exact path (8), which
+    # would give the same bits
+    fl = ag.select_row_flags(red.comp, n, d).tolist()
+    assert all(f & 8 == 0 and f & 4 for f in fl), f"row flags {fl}: expected the fast path's tie cut"
     w = [0.75, 1.5, 1.0]
     assert_bitexact(red(rt, weights=w), oc.reduce_plain(enc, w))
     c = ag.initCompressor(f"topk:{k}", d)
     for i in range(n):
         assert_bitexact(c.compressVector(rt[i]), enc[i])
+        f = int(ag.select_row_flags(c, 1, d)[0])
+        assert f & 8 == 0 and f & 4, f"compressVector row {i}: flags {f}, expected the fast path's tie cut"
 
 
 def test_topk_few_rows_stay_on_fast_path(ag):
-    """Performance guard for the few-row path (n <= 16: sharded lists + k_cs_pass): Gaussian rows at
+    """Path guard for the few-row path (n <= 16: sharded lists + k_cs_pass): Gaussian rows at
     D = 10 M must not fall back to the exact selection (~8 ms per failed row against ~0.1 ms).  Two
     round-3 builds did: the fused uplink's interleaved item order put each of n rows' groups into
-    64 / n shards (overflow), and ambiguous ties at the K-th key (~1 row in 8) went to the exact path."""
+    64 / n shards (overflow), and ambiguous ties at the K-th key (~1 row in 8) went to the exact path.
+    Asserted on the rows' path flags (flc_select_row_flags), not on wall-clock time; the device
+    times are printed for information."""
     n, d = 8, 10_000_000
     k = d // 100
     gen = torch.Generator(device="cuda").manual_seed(9)
@@ -363,10 +405,77 @@ def test_topk_few_rows_stay_on_fast_path(ag):
         return e0.elapsed_time(e1) / reps
 
     fused = dev_ms(lambda: red(rows))
-    assert fused < 3.0, f"fused {n}-row uplink {fused:.2f} ms: a row took the exact path"
+    fl = ag.select_row_flags(red.comp, n, d).tolist()
+    assert all(f & 8 == 0 for f in fl), f"fused {n}-row uplink: row flags {fl} (8 = exact path)"
+    times = []
     for i in range(n):
-        one = dev_ms(lambda: c.compressVector(rows[i]))
-        assert one < 2.0, f"compressVector of row {i}: {one:.2f} ms: the exact path"
+        times.append(dev_ms(lambda: c.compressVector(rows[i])))
+        f = int(ag.select_row_flags(c, 1, d)[0])
+        assert f & 8 == 0, f"compressVector of row {i}: flags {f} (8 = exact path)"
+    print(f"fused {n}-row uplink {fused:.3f} ms; compressVector " + " ".join(f"{t:.3f}" for t in times) + " ms")
+
+
+@pytest.mark.parametrize("kind", ["normal", "heavy", "ties", "fewnz"])
+def test_topk_c3_variant_vs_oracle(ag, kind):
+    """The C3 bench's own TopK kernel variant: many rows (n > 16) with
+    n * D >= 64 Mi take k_topk_filter_fast<16, 4> (4-chunk work items) in 4 tail row groups, each
+    group's select and exact fallback on the side stream under the next group's filter.  n = 256,
+    D = 300 007 (ragged last chunk and group), K = 1 %: bit-exact vs the oracle, weighted, through
+    both entry points; the profile counters show the 4-chunk filter ran (4 launches per call) and,
+    for normal / heavy-tailed rows, the path flags show no row fell back to the exact path."""
+    n, d = 256, 300_007
+    k = math.ceil(0.01 * d)
+    g = np.random.default_rng([n, d, len(kind), 4])
+    rows = _topk_rows(kind, n, d, g)
+    enc = _topk_enc(rows, k)
+    w = [float(v) for v in g.uniform(0.5, 2.0, n)]
+    red = ag.UplinkReducer(ag.initCompressor("topk:1%", d))
+    assert red.comp.K == k
+    rt = torch.from_numpy(rows).cuda()
+    with _FilterVariants() as fv:
+        got = red(rt)
+    assert (fv.g4, fv.g2) == (4, 0), f"filter variants g4={fv.g4} g2={fv.g2}: not the C3 bench's path"
+    assert_bitexact(got, oc.reduce_plain(enc))
+    if kind in ("normal", "heavy"):
+        fl = np.asarray(ag.select_row_flags(red.comp, n, d))
+        assert not np.any(fl & 8), f"{int(np.sum((fl & 8) != 0))} rows took the exact path"
+    want_w = oc.reduce_plain(enc, w)
+    assert_bitexact(red(rt, weights=w), want_w)
+    with _FilterVariants() as fv:
+        got = red([rt[i] for i in range(n)], weights=w)
+    assert (fv.g4, fv.g2) == (4, 0)
+    assert_bitexact(got, want_w)
+
+
+@pytest.mark.parametrize("m", [448, 511, 512, 513, 576, 700])
+def test_topk_4chunk_group_staging_capacity(ag, m):
+    """The 512-entry LDS staging of a 4-chunk group (the C3 variant, n = 17 > 16 rows, n * D >=
+    64 Mi): row i holds exactly K nonzeros, m_i of them in its first group (elements 0..16383), the
+    rest spread thinly; the sample's threshold then falls in the zeros, so the candidates are the
+    nonzeros and group 0 stages exactly m_i of them — just below, at or past the staging.  A group
+    that fits stays on the fast path; one past 512 overflows (spare slots) and its row is redone
+    exactly (flag 8).  Bit-exact vs the oracle either way."""
+    n, d = 17, 4_000_000
+    k = d // 100
+    g = np.random.default_rng([m, 17])
+    rows = np.zeros((n, d), dtype=np.float32)
+    counts = [m if i % 2 == 0 else 256 for i in range(n)]     # odd rows: a quiet first group
+    for i in range(n):
+        head = g.choice(16384, size=counts[i], replace=False)
+        tail = 16384 + g.choice(d - 16384, size=k - counts[i], replace=False)
+        idx = np.concatenate([head, tail])
+        rows[i, idx] = (g.standard_normal(idx.size) + np.sign(g.standard_normal(idx.size)) * 0.1).astype(np.float32)
+    assert np.all(np.count_nonzero(rows, axis=1) == k)
+    enc = _topk_enc(rows, k)
+    red = ag.UplinkReducer(ag.initCompressor(f"topk:{k}", d))
+    with _FilterVariants() as fv:
+        got = red(torch.from_numpy(rows).cuda())
+    assert fv.g4 >= 1 and fv.g2 == 0, f"filter variants g4={fv.g4} g2={fv.g2}"
+    assert_bitexact(got, oc.reduce_plain(enc))
+    fl = ag.select_row_flags(red.comp, n, d).tolist()
+    for i in range(n):
+        exact = counts[i] > 512
+        assert bool(fl[i] & 8) == exact, f"row {i} ({counts[i]} in group 0): flags {fl[i]}"
 
 
 def test_topk_c3_row_size(ag):

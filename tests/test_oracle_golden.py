@@ -302,3 +302,23 @@ def test_oracle_row_size_vs_reference(name):
     pref = np.uint32(m["pnorm_bits"]).view(np.float32)
     assert sha(o.compress(x, pnorm=pref)) == m["out_sha"]
     assert int(np.float32(o.norm(x)).view(np.uint32)) == m["exact_norm_bits"]
+
+
+@pytest.mark.parametrize("kind", ["normal", "ties", "zeros", "nan_inf", "fewnz"])
+@pytest.mark.parametrize("d,k", [(1, 1), (17, 5), (4096, 41), (100003, 1000), (50000, 50000)])
+def test_oracle_topk_fast_equals_sort(kind, d, k):
+    """topk_indices_fast (selection; the large-row GPU tests) is the same set as topk_indices (the
+    full lexsort restatement of compressors.py:330-335 with the lowest-index tie rule)."""
+    g = np.random.default_rng([d, k, len(kind)])
+    x = g.standard_normal(d).astype(np.float32)
+    if kind == "ties":
+        x = (g.integers(-3, 4, d) * 0.5).astype(np.float32)
+    elif kind == "zeros":
+        x[:] = 0.0
+        x[::97] = 1.0
+    elif kind == "nan_inf":
+        x[d // 2] = np.inf
+        x[d // 3] = -np.nan
+    elif kind == "fewnz":
+        x[x.size // 50:] = 0.0
+    np.testing.assert_array_equal(oc.topk_indices_fast(x, k), oc.topk_indices(x, k))

@@ -3,7 +3,7 @@
 
 The rows' physical placement moves a whole step by up to ~10 % from one allocation (one process)
 to the next, which swamps most kernel changes when variants run in separate
-processes.  Here every variant (flpytorch_amd/libflcodec_<tag>.so, "prod" = the product library)
+processes.  Here every variant (abvar/libflcodec_<tag>.so, "prod" = the product library)
 is loaded into one process (_lib.open_variant / _lib.use) and timed on the same rows, rounds
 interleaved: the per-variant medians compare kernels at matched placement.  Each round also times
 a plain read of the rows (the serverGradient fold) as the allocation's ceiling.
