@@ -93,6 +93,9 @@ constexpr int DS_RINGC = 4;                // compat filter ring (x + u: 24 B pe
 #define FLC_DS_PL 0
 #endif
 constexpr int DS_PLS = 10;
+#ifndef FLC_DS_RW
+#define FLC_DS_RW 8                  // k_ds_resolve: candidate windows (64 each) gathered up front
+#endif
 
 // One entry of the fold's lists (u16): half-chunk-local index (11 bits) | sign << 11 | level << 12;
 // its contribution is copysign(levels[level], sign) * norm — C(x) exactly as the encode forms it.
@@ -224,8 +227,9 @@ __global__ __launch_bounds__(DS_SNT) void k_ds_sample(RowSrc rows, int64_t n, in
 // in-order vmcnt queue of the load stream.  The tab gets the sure entries' (offset, count) per
 // 2048-element half chunk (the fold's tile).
 // ------------------------------------------------------------------------------------------
-// PROBE (tuning build only, FLC_DS_PROBE; outputs NOT valid): 1 fp32 norm; 2 no candidate staging;
-// 3 loads + norm only; 4 the draw's group hash without its multiplies
+// PROBE (tuning / A/B builds only, FLC_DS_PROBE or -DFLC_DS_PROBE_DEF; outputs NOT valid): 1 fp32
+// norm; 2 no candidate staging; 3 loads + norm only; 4 the draw's group hash without its
+// multiplies; 5 exec-narrowed staging without a branch; 6 staging without the classification
 //
 // COMPAT: the draws are the caller's float64 uniforms u (the reference's numpy stream, [n][uld]),
 // read in the same single pass (12 B per element).  A lane then holds elements {2l, 2l+1, 128 + 2l,
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
             const float q0 = sload(ws.q0 + row), q1 = sload(ws.q1 + row);
             const uint32_t rk2 = rk ^ 0x27D4EB2Fu;
             const uint32_t j0 = (uint32_t)(gi * (FGS * CHUNK));
-            const uint32_t ncl = fits ? cnt : 0u;
+            const uint32_t ncl = (fits && PROBE != 6) ? cnt : 0u;     // probe 6: no classification
             for (uint32_t e0 = 0; e0 < ncl; e0 += 64) {
                 const uint32_t e = e0 + (uint32_t)lane;
                 const bool v = e < ncl;
@@ -612,6 +616,240 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
         row = nrow;
         c = nc;
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Filter v2 (device draws, the product path): the same single pass, with each item's
+// classification moved into the NEXT item's streaming loop.  Probes on one allocation (round 4):
+// the classification epilogue cost k_ds_filter 1.25 ms of 9.69 at C4 (without it 8.44; loads +
+// norm alone 8.36) — while a wave classifies it issues no loads, and the issue-bound epilogue
+// grows on boxes that run a lower sustained clock.  Here the staging is double-buffered: item i
+// is staged into buffer `par` while item i-1's candidates (buffer par ^ 1) are classified one
+// 64-entry batch at a time at 8 fixed points of the loop (between load issues), and item i-1's
+// fixed store sequence goes out at the end of item i.  Same entries, same lists, same bits.
+// ------------------------------------------------------------------------------------------
+#ifndef FLC_DS2_WPE
+#define FLC_DS2_WPE 4                // LDS: 40 KB per block, 4 blocks per CU
+#endif
+template <int RING, int GCAP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS2_WPE))) void k_ds_filter2(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws, UniformSrc) {
+    constexpr int FGS = DS_FGS, NH = DS_NH;
+    static_assert(FGS == 2 && NH == 4 && GCAP == 512 && DS_HCAP == 128, "batch points / copy-out layout");
+    static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
+    constexpr int NB = GCAP / 64;                          // classification batches of one item
+    constexpr int DS_ITEM_STORES = 4 + GCAP / 128;          // partial, itm, tab, sure and ambiguous copy-outs
+    __shared__ __attribute__((aligned(16))) uint2 stage[2][4][GCAP + 64];
+    __shared__ __attribute__((aligned(16))) uint16_t stage16[4][GCAP];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t G = ws.G;
+    const int64_t items = rn * G;
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t it = (int64_t)blockIdx.x * 4 + wv;
+    if (it >= items) return;
+    const uint32_t lphi = (uint32_t)lane * 0x9E3779B1u;    // group index g = c*1024 + 64 L + lane
+    uint16_t* s16 = stage16[wv];
+    float4 ring[RING];
+    auto item_at = [&](int64_t t, int64_t& r, int64_t& g) {   // k_ds_filter's item order
+        const int64_t blk = t / (rb * G), rem = t - blk * rb * G;
+        const int64_t bn = min(rb, rn - blk * rb);
+        g = rem / bn;
+        r = r0 + blk * rb + (rem - g * bn);
+    };
+    int64_t row, gi0;
+    item_at(it, row, gi0);
+    int64_t c = gi0 * FGS;
+    auto rs = chunk_rsrc(rows.row_s(row), c * CHUNK, d);
+#pragma unroll
+    for (int L = 0; L < RING - 1; ++L) {
+        ring[L] = load_q(rs, lane, L);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    {
+        const auto nd = __builtin_amdgcn_make_buffer_rsrc(ws.enta, (short)0, 0, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < DS_ITEM_STORES; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, nd, lane * 4, k * 256, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // the previous item (pv): its row, item, candidate count, norm partial, classification scales
+    bool pv = false, pfits = true;
+    int64_t prow = 0, pgi = 0;
+    uint32_t pncl = 0, prk = 0;
+    double pa2 = 0.0;
+    float pq0 = 0.f, pq1 = 0.f;
+    uint32_t hs[NH], na = 0;                               // its classification counters
+#pragma unroll
+    for (int u = 0; u < NH; ++u) hs[u] = 0;
+    int par = 0;
+    // batch b of the previous item's candidates: sure entries to s16 (half h's at h * DS_HCAP),
+    // ambiguous ones compacted in place in its staging (a batch reads its 64 slots before it
+    // writes lower ones); k_ds_filter's classification, verbatim
+    auto classify = [&](int b) {
+        uint2* sgp = stage[par ^ 1][wv];
+        const uint32_t e = (uint32_t)(b * 64 + lane);
+        const bool v = e < pncl;
+        const uint2 en = v ? sgp[e] : make_uint2(0u, 0u);
+        const float x = __uint_as_float(en.y), ax = fabsf(x);
+        const uint32_t loc = en.x & 0x1FFFu;
+        const uint32_t j0 = (uint32_t)(pgi * (FGS * CHUNK));
+        const uint32_t hi8 = ds_hi8(j0 + loc, prk);
+        const uint32_t h24 = (hi8 << 16) | (fmix32(colbase(j0 + loc) + (prk ^ 0x27D4EB2Fu)) >> 16);   // h >> 8
+        const float hf = (float)h24 * 0x1p-24f, hfu = (float)(h24 + 1u) * 0x1p-24f;
+        const bool inl = ax * pq0 <= 1.0f - 0x1p-18f;
+        const bool nz = v && !(x == 0.f);
+        const bool sure = nz && inl && fmaf(ax, pq1, hf) >= 1.0f + 0x1p-20f;
+        const bool drop = !nz || (inl && fmaf(ax, pq0, hfu) < 1.0f - 0x1p-20f);
+        const bool amb = !sure && !drop;
+        const uint32_t u = loc >> 11;
+        uint32_t pin = 0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const uint64_t mh = __ballot(sure && u == (uint32_t)h);
+            const uint32_t ph = __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, hs[h]));
+            pin = u == (uint32_t)h ? ph : pin;
+            hs[h] += (uint32_t)__popcll(mh);
+        }
+        if (sure && pin < (uint32_t)DS_HCAP)
+            s16[u * DS_HCAP + pin] = (uint16_t)((loc & (HCHUNK - 1)) | ((en.y >> 31) << 11) | (1u << 12));
+        const uint64_t ma = __ballot(amb);
+        const uint32_t pa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, na));
+        if (amb) sgp[pa] = make_uint2(loc | (hi8 << 13), en.y);     // k_ds_resolve's entry
+        na += (uint32_t)__popcll(ma);
+    };
+    // the previous item's stores: k_ds_filter's fixed sequence, every store a range-checked buffer
+    // store (no previous item: all dropped), so the vmcnt queue has the same shape every time
+    auto finish = [&]() {
+        bool ovf = !pfits;
+#pragma unroll
+        for (int u = 0; u < NH; ++u) ovf |= hs[u] > (uint32_t)DS_HCAP;
+        typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        {
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.partial + prow * G + pgi, (short)0, pv ? 8 : 0, 0x00020000);
+            const uint64_t ab = __builtin_bit_cast(uint64_t, pa2);
+            const u2v v2 = {(unsigned)ab, (unsigned)(ab >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(v2, od, 0, 0, 0);
+        }
+        {
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.itm + pgi * n + prow, (short)0, pv ? 4 : 0, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(ovf ? DS_OVF : na, od, 0, 0, 0);
+        }
+        {
+            // halves past the row end land in the tab's padding rows (G * NH >= H)
+            const uint32_t u = (uint32_t)lane & (NH - 1);
+            uint32_t hc = 0;
+#pragma unroll
+            for (int v = 0; v < NH; ++v) hc = (uint32_t)v == u ? hs[v] : hc;
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.tabs + pgi * NH * n + prow, (short)0,
+                                                              pv ? (int)(((NH - 1) * n + 1) * 8) : 0, 0x00020000);
+            const u2v v2 = {0u, ovf ? 0u : hc};
+            __builtin_amdgcn_raw_buffer_store_b64(v2, od, u * (uint32_t)n * 8u, 0, 0);
+        }
+        {
+            const uint32_t u = (uint32_t)lane >> 4, k8 = ((uint32_t)lane & 15u) * 8u;
+            uint32_t hc = 0;
+#pragma unroll
+            for (int v = 0; v < NH; ++v) hc = (uint32_t)v == u ? hs[v] : hc;
+            const bool put = pv && !ovf && k8 < hc;
+            const uint32_t hstride = (uint32_t)n * (DS_HCAP * 2);               // bytes
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.ent16 + (pgi * NH * n + prow) * DS_HCAP, (short)0,
+                                                              (int)((NH - 1) * hstride + DS_HCAP * 2), 0x00020000);
+            const uint4 v = reinterpret_cast<const uint4*>(s16)[lane];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), od, put ? u * hstride + k8 * 2u : 0x7FFFFFF0u, 0, 0);
+        }
+        {
+            const uint32_t nrec = (pv && !ovf) ? ((na + 1u) & ~1u) * 8u : 0u;
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.enta + prow * ws.cap + pgi * GCAP, (short)0, (int)nrec, 0x00020000);
+            const uint4* sq = reinterpret_cast<const uint4*>(stage[par ^ 1][wv]);
+#pragma unroll
+            for (int k = 0; k < GCAP / 128; ++k) {
+                const uint4 v = sq[k * 64 + lane];
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), od, (k * 64 + lane) * 16, 0, 0);
+            }
+        }
+    };
+    while (it < items) {
+        const float qc = sload(ws.qc + row);
+        const uint32_t rk = sload(ws.rk + row);
+        const int64_t gi = c / FGS;
+        const int64_t nit = it + stride;
+        uint32_t cnt = 0;
+        double a2 = 0.0;
+        int64_t nrow = row, nc = c;
+        const uint32_t sla = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint2*)stage[par][wv]);
+        na = 0;
+#pragma unroll
+        for (int u = 0; u < NH; ++u) hs[u] = 0;
+#pragma unroll
+        for (int sub = 0; sub < FGS; ++sub, ++c) {
+            const int64_t j0 = c * CHUNK;
+            __amdgpu_buffer_rsrc_t rsn;
+            if (sub + 1 < FGS) {
+                rsn = chunk_rsrc(rows.row_s(row), j0 + CHUNK, d);
+            } else if (nit < items) {
+                int64_t ngi;
+                item_at(nit, nrow, ngi);
+                nc = ngi * FGS;
+                rsn = chunk_rsrc(rows.row_s(nrow), nc * CHUNK, d);
+            } else {
+                rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(row)), (short)0, 0, 0x00020000);
+            }
+            uint32_t jb = (uint32_t)lane * 4u + (uint32_t)sub * CHUNK;
+            asm volatile("" : "+v"(jb));
+            const uint32_t gb = lphi + (uint32_t)(c * 1024) * 0x9E3779B1u + rk;
+#pragma unroll
+            for (int L = 0; L < 16; ++L) {
+                const int P = L + RING - 1;
+                ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
+                const float4 x = ring[L % RING];
+                const uint32_t hg = gmix(gb + (uint32_t)(L * 64) * 0x9E3779B1u);
+                const float vq[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    a2 = fma((double)vq[q], (double)vq[q], a2);
+                    const float hi = (float)((hg >> (8 * q)) & 0xFFu);
+                    const bool f = fmaf(fabsf(vq[q]), qc, hi) > DS_QT;
+                    const uint64_t m = __ballot(f);
+                    if (f) {
+                        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        uint32_t sb = sla + min(cnt, (uint32_t)GCAP) * 8u;
+                        asm volatile("" : "+s"(sb));
+                        const uint32_t la = sb + pre * 8u;
+                        asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(jb + (uint32_t)(L * 256 + q)),
+                                     "v"(__float_as_uint(vq[q])) : "memory");
+                    }
+                    cnt += (uint32_t)__popcll(m);
+                }
+                asm volatile("" : "+v"(a2));
+                // the previous item's batches, between load issues (8 points cover GCAP)
+                if ((L & 3) == 1) {
+                    const int b = sub * 4 + (L >> 2);
+                    if ((uint32_t)(b * 64) < pncl) classify(b);
+                }
+            }
+            rs = rsn;
+        }
+        a2 = wave_sum(a2);
+        finish();
+        prow = row; pgi = gi; pfits = cnt <= GCAP; pncl = pfits ? cnt : 0u; pa2 = a2; prk = rk;
+        pq0 = sload(ws.q0 + row); pq1 = sload(ws.q1 + row);
+        pv = true;
+        // the copy-out reads and the classification precede the next item's staging writes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        par ^= 1;
+        it = nit;
+        row = nrow;
+        c = nc;
+    }
+    // the last item: classify, then its stores
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    na = 0;                                                  // (its staging: buffer par ^ 1)
+#pragma unroll
+    for (int u = 0; u < NH; ++u) hs[u] = 0;
+    for (int b = 0; b < NB; ++b)
+        if ((uint32_t)(b * 64) < pncl) classify(b);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    finish();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -807,15 +1045,38 @@ __global__ __launch_bounds__(256) void k_ds_resolve(int64_t n, int64_t r0, int64
             const uint2 v = ws.enta[ei];                          // lanes past the total: entry 0 (ignored)
             return v;
         };
+        // The first RW windows' owners and candidate loads are all issued before any is encoded
+        // (their gathers from 64 rows' regions overlap instead of costing one round trip each);
+        // windows past RW are fetched one ahead.
+        constexpr int RW = FLC_DS_RW;
+        uint32_t kw[RW];
+        uint2 ew[RW];
+#pragma unroll
+        for (int w = 0; w < RW; ++w) {
+            kw[w] = 0u;
+            ew[w] = make_uint2(0u, 0u);
+            if ((uint32_t)w * 64u < total) { kw[w] = owner((uint32_t)w * 64u); ew[w] = fetch((uint32_t)w * 64u, kw[w]); }
+        }
         uint32_t kc = 0;
         uint2 enc = make_uint2(0u, 0u);
-        if (total > 0u) { kc = owner(0u); enc = fetch(0u, kc); }
+        if ((uint32_t)RW * 64u < total) { kc = owner((uint32_t)RW * 64u); enc = fetch((uint32_t)RW * 64u, kc); }
         for (uint32_t t0 = 0; t0 < total; t0 += 64) {
             const uint32_t t = t0 + (uint32_t)lane;
             const bool tv = t < total;
-            const uint32_t k = kc;
-            const uint2 en = tv ? enc : make_uint2(0u, 0u);
-            if (t0 + 64u < total) { kc = owner(t0 + 64u); enc = fetch(t0 + 64u, kc); }
+            const uint32_t wi = t0 >> 6;
+            uint32_t k = kc;
+            uint2 en = enc;
+            if (wi < (uint32_t)RW) {
+#pragma unroll
+                for (int w = 0; w < RW; ++w)
+                    if ((uint32_t)w == wi) { k = kw[w]; en = ew[w]; }
+            } else if (t0 + 64u < total) {
+                const uint32_t kn = owner(t0 + 64u);
+                const uint2 nn = fetch(t0 + 64u, kn);
+                k = kc; en = enc;
+                kc = kn; enc = nn;
+            }
+            en = tv ? en : make_uint2(0u, 0u);
             const int64_t rk_ = irow[wv][k];
             const uint32_t gk = igi[wv][k];
             const float x = __uint_as_float(en.y);
@@ -883,6 +1144,9 @@ __device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r
     return m;
 }
 
+#ifndef FLC_DS_MASKLD
+#define FLC_DS_MASKLD 0
+#endif
 #ifndef FLC_DS_AW
 #define FLC_DS_AW 1                  // waves per fold workgroup (LDS: one 8 KB tile per wave)
 #endif
@@ -932,8 +1196,15 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
         auto fetch = [&](const DsMeta& m, int q, int64_t row, int slot) {
             const uint32_t cnt = __builtin_amdgcn_readlane(m.cnt, q);
             const uint16_t* p = cnt ? ws.ent16 + (h * n + row) * DS_HCAP : ws.ent16;
+#if FLC_DS_MASKLD
+            // only the lanes of the list's entries load (the region is 256 B, a list ~80 B)
+            uint32_t v = NONE;
+            if ((uint32_t)lane < cnt) v = __builtin_nontemporal_load(p + lane);
+            ra[slot] = v;
+#else
             const uint32_t v = p[lane];
             ra[slot] = (uint32_t)lane < cnt ? v : NONE;
+#endif
         };
         // (LDS float atomic adds instead of the read-modify-write — one wave's LDS operations run
         // in issue order, so the row order would hold — measured 1.34 against 0.51 ms at C4)
@@ -1066,10 +1337,16 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
 // Filter grid.  The product build always takes the default; a -DFLC_TUNING build reads the
 // A/B switches once per process (FLC_DS_GRID=res launches a resident-only grid; FLC_DS_GRIDPCT=p
 // caps it at p % of the resident blocks when row groups run).
+#ifndef FLC_DS_V2
+#define FLC_DS_V2 0                  // device-RNG filter: classification pipelined into the next item (k_ds_filter2)
+#endif
+#ifndef FLC_DS_PROBE_DEF
+#define FLC_DS_PROBE_DEF 0           // A/B variant builds only (a probe's outputs are NOT valid)
+#endif
 struct DsVariant { bool resident; int gridpct; int probe; int64_t rb; int cring; };
 static const DsVariant& ds_variant() {
     static const DsVariant v = [] {
-        DsVariant r{false, 100, 0, DS_RB, DS_RINGC};
+        DsVariant r{false, 100, FLC_DS_PROBE_DEF, DS_RB, DS_RINGC};
         if (const char* e = tuning_env("FLC_DS_CRING")) r.cring = atoi(e);
         if (const char* e = tuning_env("FLC_DS_RB")) r.rb = std::max<int64_t>(1, atoll(e));
         if (const char* e = tuning_env("FLC_DS_PROBE")) r.probe = atoi(e);
@@ -1178,7 +1455,8 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         auto kern = compat ? (v.cring == 8 ? k_ds_filter<8, DS_GCAP, 0, true> : k_ds_filter<DS_RINGC, DS_GCAP, 0, true>)
                   : v.probe == 1 ? k_ds_filter<16, DS_GCAP, 1> : v.probe == 2 ? k_ds_filter<16, DS_GCAP, 2>
                   : v.probe == 3 ? k_ds_filter<16, DS_GCAP, 3> : v.probe == 4 ? k_ds_filter<16, DS_GCAP, 4>
-                  : v.probe == 5 ? k_ds_filter<16, DS_GCAP, 5> : k_ds_filter<16, DS_GCAP>;
+                  : v.probe == 5 ? k_ds_filter<16, DS_GCAP, 5> : v.probe == 6 ? k_ds_filter<16, DS_GCAP, 6>
+                  : FLC_DS_V2 ? k_ds_filter2<16, DS_GCAP> : k_ds_filter<16, DS_GCAP>;
         int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
         if (v.resident || (K > 1 && v.gridpct < 100)) {
             int per = 0, dev = 0, cus = 0;

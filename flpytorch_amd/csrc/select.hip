@@ -64,6 +64,7 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* cstate;     // [N][4] few-row candidate select: shift, prefix, krem, stage (k_cs_pass)
     uint32_t* carrive;    // [N * RCS] its per-row arrival counters
     uint32_t* shcnt;      // [N][CS_SH * RCS] few rows: the filter's reservation counters, one per shard
+    uint32_t* zm;         // [C][CHUNK / 32] k_chunk_accum (one-wave blocks): a fold job's kept-column mask
     int64_t cap;
 };
 
@@ -682,6 +683,12 @@ template <int RING, int FGS, bool ZF = false>
 #ifndef FLC_TK_RING
 #define FLC_TK_RING 16               // loads in flight per wave (ring registers: 4 x RING VGPRs)
 #endif
+#ifndef FLC_TK_COPY4
+#define FLC_TK_COPY4 1               // TopK filter copy-out: 16-B stores of whole quads
+#endif
+#ifndef FLC_TK_PROBE
+#define FLC_TK_PROBE 0               // A/B cost probes (outputs NOT valid): 1 no staging writes, 2 no copy-out, 3 loads only
+#endif
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
@@ -694,7 +701,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
     // per entry; the 64 spare slots take a wave-instruction starting at GCAP, i.e. an overflow)
     constexpr int SROW = GCAP + 64;
     static_assert((SROW * 4) % 256 == 0, "value block offset in 256-byte units");
-    __shared__ uint32_t st[2][4][2 * SROW];
+    __shared__ __attribute__((aligned(16))) uint32_t st[2][4][2 * SROW];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: keeps the item walk in SGPRs
     const int64_t C = nchunks(d);
@@ -751,7 +758,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
             ws.tab[(pc0 + lane) * n + prow] = make_uint2(base + off, fits ? cc : 0u);
         }
         if (!fits && lane == 0) atomicOr(&ws.flags[prow], F_OVERFLOW);
-        if (fits) {
+#if FLC_TK_COPY4
+        {
+            // Copy-out as 16-B stores of 4 entries a lane (the group's whole quads) plus the last
+            // partial quad's entries as 4-B stores: a FIXED sequence of 2 GCAP / 256 + 2
+            // range-checked buffer stores (none written when the group did not fit) instead of
+            // 2 GCAP / 64 exec-masked 4-B stores — the copy-out cost the filter 0.5 ms of 6.9 per
+            // C3 step (probe, same allocation).  The list position is any dword: the 16-B
+            // stores need only dword alignment.
+            const uint32_t* si = st[pb][wv];
+            const uint32_t* sv = st[pb][wv] + SROW;
+            const uint32_t nrec = (fits && FLC_TK_PROBE != 2) ? ptot * 4u : 0u;
+            const auto di = __builtin_amdgcn_make_buffer_rsrc(ws.ent_idx + prow * ws.cap + base, (short)0, (int)nrec, 0x00020000);
+            const auto dv = __builtin_amdgcn_make_buffer_rsrc(ws.ent_val + prow * ws.cap + base, (short)0, (int)nrec, 0x00020000);
+            typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+            const uint32_t nq = ptot >> 2;
+#pragma unroll
+            for (int k = 0; k < GCAP / 256; ++k) {
+                const uint32_t q = (uint32_t)(k * 64 + lane);
+                const uint4 a = reinterpret_cast<const uint4*>(si)[q];
+                const uint4 b = reinterpret_cast<const uint4*>(sv)[q];
+                const uint32_t off = q < nq ? q * 16u : 0x7FFFFFF0u;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), di, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), dv, off, 0, 0);
+            }
+            const uint32_t e = nq * 4u + (uint32_t)(lane & 3);          // the partial quad (range-checked)
+            const uint32_t off = lane < 3 ? e * 4u : 0x7FFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b32(si[e], di, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(sv[e], dv, off, 0, 0);
+        }
+#else
+        if (fits && FLC_TK_PROBE != 2) {
             const uint32_t* si = st[pb][wv];
             const float* sv = reinterpret_cast<const float*>(st[pb][wv] + SROW);
             uint32_t* oi = ws.ent_idx + prow * ws.cap + base;
@@ -764,6 +801,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 if (e < ptot) { oi[e] = si[e]; ov[e] = sv[e]; }
             }
         }
+#endif
     };
     while (it < items) {
         // key >= max(T, 1): the loads past the row end return +0 (key 0), so no per-element range
@@ -815,9 +853,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 const float vq[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    if (FLC_TK_PROBE == 3) { cnt += __float_as_uint(vq[q]) == 0x7F800001u ? 1u : 0u; continue; }
                     const bool f = mag_key(vq[q]) >= T;
                     const uint64_t m = __ballot(f);
-                    if (f) {
+                    if (FLC_TK_PROBE != 1 && f) {
                         // slot = min(cnt, GCAP) + entries in lower lanes (< GCAP + 64): exact while
                         // the group fits; past GCAP it overflows (its row takes the exact path) and
                         // the writes land in the spare slots.  The scalar part folded into the LDS
@@ -1069,7 +1108,8 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
             ws.thr[row] = thr;
             ws.krem[row] = krem;
             ws.rowcnt[row * RCS] = base;
-            ws.flags[row] = F_EXACT;
+            // the reason the fast path failed stays readable (flc_select_row_flags)
+            ws.flags[row] = F_EXACT | (ws.flags[row] & (F_OVERFLOW | F_SHORT));
         }
         __syncthreads();
     }
@@ -1378,6 +1418,9 @@ __global__ __launch_bounds__(RK_FTHR) void k_randk_fine(RowSrc rows, int64_t n, 
 // flight while a row is folded (a ring of AP register slots, 2 x 64 entries per row), so the
 // wave never waits on a dependent tab -> entries round trip.
 // ------------------------------------------------------------------------------------------
+#ifndef FLC_CA_WPB1
+#define FLC_CA_WPB1 0                // k_chunk_accum over whole chunks: one-wave workgroups
+#endif
 #ifndef FLC_CA_AP
 #define FLC_CA_AP 8
 #endif
@@ -1467,20 +1510,86 @@ __device__ void resolve_neg_zero(float* tl, uint32_t* rm, const SelWs& ws, int64
     }
 }
 
+// resolve_neg_zero for one-wave workgroups whose LDS holds only the tile: the -0 column masks
+// live in registers (word k of the tile's TS / 32 in lane k % 64), a row's kept columns are OR-ed
+// into the job's global scratch `rm` (TS / 32 words) and read back at L2 (atomic reads: no stale
+// L1 line).  Same rule, same bits; it runs once per job and usually stops after one row.
+template <int TS>
+__device__ void resolve_neg_zero_g(float* tl, uint32_t* rm, const SelWs& ws, int64_t c, int64_t n, uint32_t cbase,
+                                   int64_t len, const float* w, int lane) {
+    constexpr int NW = TS / 32;                        // mask words (32 columns each)
+    constexpr int WL = (NW + 63) / 64;                 // mask words per lane (word k = lane + 64 j)
+    uint32_t z0[WL], zc[WL];
+#pragma unroll
+    for (int j = 0; j < WL; ++j) z0[j] = 0u;
+    bool any = false;
+#pragma unroll 4
+    for (int k = 0; k < TS / 64; ++k) {
+        const int64_t i = (int64_t)k * 64 + lane;
+        const uint64_t b = __ballot(i < len && __float_as_uint(tl[i]) == 0x80000000u);
+        const int w0 = 2 * k, w1 = 2 * k + 1;          // words of columns 64 k .. 64 k + 63
+#pragma unroll
+        for (int j = 0; j < WL; ++j) {
+            if (lane == (w0 & 63) && (w0 >> 6) == j) z0[j] = (uint32_t)b;
+            if (lane == (w1 & 63) && (w1 >> 6) == j) z0[j] = (uint32_t)(b >> 32);
+        }
+        any |= b != 0ull;
+    }
+    if (!any) return;
+#pragma unroll
+    for (int j = 0; j < WL; ++j) zc[j] = z0[j];
+    for (int64_t r = 0; r < n; ++r) {
+        if (w && (__float_as_uint(w[r]) >> 31)) continue;      // its skipped term is -0: no constraint
+#pragma unroll
+        for (int j = 0; j < WL; ++j) if (lane + 64 * j < NW) rm[lane + 64 * j] = 0u;
+        __threadfence_block();
+        const RowMeta m = load_meta(ws, c, n, r, w);
+        const uint32_t mode = m.mode, T = m.thr, cut = m.cut;
+        for (uint32_t e = (uint32_t)lane; e < m.te.y; e += 64) {
+            const uint32_t ix = ws.ent_idx[r * ws.cap + m.te.x + e];
+            const uint32_t key = mag_key(ws.ent_val[r * ws.cap + m.te.x + e]);
+            const uint32_t loc = ix - cbase;
+            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut)))
+                atomicOr(&rm[loc >> 5], 1u << (loc & 31));
+        }
+        __threadfence_block();
+        bool left = false;
+#pragma unroll
+        for (int j = 0; j < WL; ++j) {
+            if (lane + 64 * j < NW) zc[j] &= atomicOr(&rm[lane + 64 * j], 0u);
+            left |= zc[j] != 0u;
+        }
+        if (__ballot(left) == 0ull) break;
+    }
+#pragma unroll
+    for (int j = 0; j < WL; ++j) {
+        uint32_t dead = z0[j] & ~zc[j];
+        while (dead) {
+            const int b = __builtin_ctz(dead);
+            dead &= dead - 1u;
+            tl[(lane + 64 * j) * 32 + b] = 0.f;
+        }
+    }
+}
+
 // TS < CHUNK: a wave owns TS columns of a chunk (CHUNK / TS waves read the same lists and each
 // folds its part): a smaller LDS tile per wave, so more waves per CU hide the list latency.
-template <bool ASSIGN, int TS = CHUNK, bool W = true>
-__global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
-                                                     float wt, float* __restrict__ out) {
+// WPB = 1 (whole chunks): one-wave workgroups holding only their 16 KB tile, so ten fit a CU's
+// 160 KB and every chunk of a 10 M row (2442) has its wave resident at once — with 4-wave blocks
+// (67.5 KB with the masks) two fit a CU, 2048 chunk waves ran and the last 394 formed a second
+// round of the same length.
+template <bool ASSIGN, int TS = CHUNK, bool W = true, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WPB == 1 ? 3 : 1))) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
+                                                          float wt, float* __restrict__ out) {
     constexpr int PARTS = CHUNK / TS;
-    __shared__ __attribute__((aligned(16))) float tile[4][TS];
-    __shared__ uint32_t zmask[4][TS / 32];
+    __shared__ __attribute__((aligned(16))) float tile[WPB][TS];
+    __shared__ uint32_t zmask[WPB == 1 ? 1 : WPB][WPB == 1 ? 1 : TS / 32];
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = WPB == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t C = nchunks(d);
     float* tl = tile[wv];
     const int64_t nb = (n + 63) / 64;                  // row batches
-    for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < C * PARTS; t += (int64_t)gridDim.x * 4) {
+    for (int64_t t = (int64_t)blockIdx.x * WPB + wv; t < C * PARTS; t += (int64_t)gridDim.x * WPB) {
         const int64_t c = t / PARTS;
         // ASSIGN (compressVector: out = zeros, out[kept] = x) stores into +0; the fold adds into -0
         for (int i = lane; i < TS; i += 64) tl[i] = ASSIGN ? 0.f : -0.f;
@@ -1573,7 +1682,10 @@ __global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs
             cur = nxt;
         }
         const int64_t len = min((int64_t)TS, d - (int64_t)cbase);
-        if (!ASSIGN) resolve_neg_zero<TS>(tl, zmask[wv], ws, c, n, cbase, len, w, lane);
+        if (!ASSIGN) {
+            if (WPB == 1) resolve_neg_zero_g<TS>(tl, ws.zm + t * (TS / 32), ws, c, n, cbase, len, w, lane);
+            else resolve_neg_zero<TS>(tl, zmask[wv], ws, c, n, cbase, len, w, lane);
+        }
         for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
     }
 }
@@ -2004,6 +2116,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     s.krem = cv.take<uint32_t>(nn);
     s.worklist = cv.take<uint32_t>(nn);
     s.nwork = cv.take<uint32_t>(4);
+    s.zm = cv.take<uint32_t>((size_t)C * (CHUNK / 32));
     if (codec == FLC_TOPK) {
         s.tieprefix = cv.take<uint32_t>((size_t)C * nn);
         s.tiecut = cv.take<uint32_t>(nn);
@@ -2089,6 +2202,9 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, (float*)nullptr);
 }
 
+#ifndef FLC_TK_EXACT_WG
+#define FLC_TK_EXACT_WG 256           // workgroups of the one exact-rows launch (one per CU)
+#endif
 // Row groups of the TopK fast path whose candidate select + exact fallback run on a side stream
 // under the next group's filter (one fold of all rows at the end), at least 64 rows each: 4
 // (measured at C3, same box, two runs each: 8.18 ms / step with 1 group, 8.15 with 2, 8.00-8.01
@@ -2216,7 +2332,12 @@ static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const
     };
     if (parts == 4) go(std::integral_constant<int, CHUNK / 4>{}, grid_stride_blocks((4 * C + 3) / 4, 8192));
     else if (parts == 2) go(std::integral_constant<int, CHUNK / 2>{}, grid_stride_blocks((2 * C + 3) / 4, 8192));
-    else go(std::integral_constant<int, CHUNK>{}, grid_stride_blocks((C + 3) / 4, 4096));
+    else if (FLC_CA_WPB1 && !assign) {
+        // one-wave workgroups (the tile alone in LDS), one per chunk
+        const int ab = grid_stride_blocks(C, 16384);
+        if (w) hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, true, 1>), dim3(ab), dim3(64), 0, st, n, d, ws, w, wt, out);
+        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, false, 1>), dim3(ab), dim3(64), 0, st, n, d, ws, w, wt, out);
+    } else go(std::integral_constant<int, CHUNK>{}, grid_stride_blocks((C + 3) / 4, 4096));
     }
     FLC_CHECK_LAUNCH("k_chunk_accum");
     return FLC_OK;
@@ -2321,13 +2442,18 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                     hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)rn), dim3(1024), 0, sside, r0, rn, K, ws);
                 else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(rn, 8192)), dim3(512), 0, sside, r0, rn, K, ws); }
                 FLC_CHECK_LAUNCH("k_cand_select");
-                if (!lone_assign) {   // rows the fast path failed (rare): exact selection, one launch
-                    ProfScope _ps("k_topk_exact_rows", sside);
-                    const int eb = grid_stride_blocks(rn, 2048);
-                    if (vec) hipLaunchKernelGGL((k_topk_exact_rows<true>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, r0, rn, d, K, ws);
-                    else hipLaunchKernelGGL((k_topk_exact_rows<false>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, r0, rn, d, K, ws);
-                    FLC_CHECK_LAUNCH("k_topk_exact_rows");
-                }
+            }
+            if (!lone_assign) {
+                // rows the fast path failed (rare): exact selection of every group's failed rows in
+                // ONE launch after the last group's select (a workgroup per row, grid-stride, rows
+                // that did not fail return at once).  Per-group launches beside the next group's
+                // filter held whole CUs (1024-thread workgroups) while doing nothing: the filters
+                // beside them ran 40-110 us slower
+                ProfScope _ps("k_topk_exact_rows", sside);
+                const int eb = grid_stride_blocks(n, FLC_TK_EXACT_WG);
+                if (vec) hipLaunchKernelGGL((k_topk_exact_rows<true>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, (int64_t)0, n, d, K, ws);
+                else hipLaunchKernelGGL((k_topk_exact_rows<false>), dim3(eb), dim3(EX_NT), 0, sside, rows, n, (int64_t)0, n, d, K, ws);
+                FLC_CHECK_LAUNCH("k_topk_exact_rows");
             }
             if (TG > 1) {
                 FLC_CHECK_HIP(hipEventRecord(cx->ev[TG], sside));

@@ -213,6 +213,29 @@ def test_sparse_dither_item_near_staging_capacity(ag, monkeypatch, big):
     assert_bitexact(got, want)
 
 
+@pytest.mark.parametrize("many", [9, 10, 11, 12, 40, 128])
+def test_sparse_dither_lane_overflow(ag, monkeypatch, many):
+    """Per-lane candidate staging (each lane of the filter's wave appends to its own column,
+    DS_PLS = 10 slots per item): `many` sure candidates among the 128 elements one lane reads in
+    an item (lane 5: elements 4*5 + 256 L + q of each chunk; lane 40 gets many // 2), the rest
+    small.  Past 10 the lane's extra candidates are re-read and appended after the compaction;
+    bit-exact vs the oracle either way (and with the pooled staging of other builds)."""
+    n, d, client0, spec = 3, 16384, 7, "qsgd:127"
+    g = np.random.default_rng(many)
+    rows = (g.standard_normal((n, d)) * 1e-3).astype(np.float32)
+    for lane, cnt in ((5, many), (40, many // 2)):
+        pos = np.array([sub * 4096 + L * 256 + lane * 4 + q for sub in range(2) for L in range(16) for q in range(4)])
+        for i in range(n):
+            pick = g.choice(pos, size=cnt, replace=False)
+            rows[i, pick] = np.where(g.random(cnt) < 0.5, -1.0, 1.0).astype(np.float32)
+    want, wn = oracle_uplink(spec, rows, client0)
+    red = ag.UplinkReducer(sparse(ag, spec, d), seed=SEED)
+    pn = torch.empty(n, device="cuda")
+    got = red(torch.from_numpy(rows).cuda(), client0=client0, pnorms_out=pn)
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)
+
+
 def compat_uniforms(n, d, g):
     """float64 draws in [0, 1) as numpy's random() makes them, with the edges planted: exact 0,
     the largest double below 1, and values a few ulps either side of 1/2."""
