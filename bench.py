@@ -819,7 +819,7 @@ def main():
                            "line_floor_GBps": round(rk_floor / (rk_ms * 1e-3) / 1e9, 1),
                            "fold_traffic_bytes": rk_traffic}
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{'_compat' if args.compat else ''}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             pj = json.load(f)

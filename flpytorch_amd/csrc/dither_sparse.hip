@@ -93,6 +93,9 @@ constexpr int DS_RINGC = 4;                // compat filter ring (x + u: 24 B pe
 #define FLC_DS_PL 0
 #endif
 constexpr int DS_PLS = 10;
+#ifndef FLC_DS_CU
+#define FLC_DS_CU 2                  // k_ds_filter: candidate batches (of 64) classified per iteration
+#endif
 #ifndef FLC_DS_RW
 #define FLC_DS_RW 8                  // k_ds_resolve: candidate windows (64 each) gathered up front
 #endif
@@ -522,44 +525,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
             const uint32_t rk2 = rk ^ 0x27D4EB2Fu;
             const uint32_t j0 = (uint32_t)(gi * (FGS * CHUNK));
             const uint32_t ncl = (fits && PROBE != 6) ? cnt : 0u;     // probe 6: no classification
-            for (uint32_t e0 = 0; e0 < ncl; e0 += 64) {
-                const uint32_t e = e0 + (uint32_t)lane;
-                const bool v = e < ncl;
-                const uint2 en = v ? sg[e] : make_uint2(0u, 0u);
-                const float x = __uint_as_float(en.y), ax = fabsf(x);
-                const uint32_t loc = en.x & 0x1FFFu;
-                uint32_t hi8 = 0;
-                float hf, hfu;                                      // hf <= draw / 2^32 (u) <= hfu
-                if constexpr (COMPAT) {
-                    const float ud = v ? sgf[e] : 0.f;
-                    hf = ud;
-                    hfu = __uint_as_float(__float_as_uint(ud) + 1u);
-                } else {
-                    hi8 = ds_hi8(j0 + loc, rk);
-                    const uint32_t h24 = (hi8 << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);   // h >> 8
-                    hf = (float)h24 * 0x1p-24f;
-                    hfu = (float)(h24 + 1u) * 0x1p-24f;
-                }
-                const bool inl = ax * q0 <= 1.0f - 0x1p-18f;
-                const bool nz = v && !(x == 0.f);
-                const bool sure = nz && inl && fmaf(ax, q1, hf) >= 1.0f + 0x1p-20f;
-                const bool drop = !nz || (inl && fmaf(ax, q0, hfu) < 1.0f - 0x1p-20f);
-                const bool amb = !sure && !drop;
-                const uint32_t u = loc >> 11;
-                uint32_t pin = 0;
+            // CU batches of 64 per iteration: their LDS reads and draw hashes are independent, so
+            // they overlap; only the compaction (ballot / mbcnt counters) runs batch after batch.
+            // All CU batches are read before any in-place write (writes go below e0 + 64 CU).
+            constexpr int CU = FLC_DS_CU;
+            for (uint32_t e0 = 0; e0 < ncl; e0 += 64 * CU) {
+                uint2 en[CU];
+                float hf[CU], hfu[CU];
+                uint32_t hi8[CU];
+                bool vv[CU];
 #pragma unroll
-                for (int h = 0; h < NH; ++h) {
-                    const uint64_t mh = __ballot(sure && u == (uint32_t)h);
-                    const uint32_t ph = __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, hs[h]));
-                    pin = u == (uint32_t)h ? ph : pin;
-                    hs[h] += (uint32_t)__popcll(mh);
+                for (int b = 0; b < CU; ++b) {
+                    const uint32_t e = e0 + (uint32_t)(b * 64 + lane);
+                    vv[b] = e < ncl;
+                    en[b] = vv[b] ? sg[e] : make_uint2(0u, 0u);
                 }
-                if (sure && pin < (uint32_t)DS_HCAP)
-                    s16[u * DS_HCAP + pin] = (uint16_t)((loc & (HCHUNK - 1)) | ((en.y >> 31) << 11) | (1u << 12));
-                const uint64_t ma = __ballot(amb);
-                const uint32_t pa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, na));
-                if (amb) sg[pa] = make_uint2(loc | (hi8 << 13), en.y);      // k_ds_resolve's entry
-                na += (uint32_t)__popcll(ma);
+#pragma unroll
+                for (int b = 0; b < CU; ++b) {
+                    const uint32_t loc = en[b].x & 0x1FFFu;
+                    hi8[b] = 0;
+                    if constexpr (COMPAT) {
+                        const uint32_t e = e0 + (uint32_t)(b * 64 + lane);
+                        const float ud = vv[b] ? sgf[e] : 0.f;
+                        hf[b] = ud;
+                        hfu[b] = __uint_as_float(__float_as_uint(ud) + 1u);
+                    } else {
+                        hi8[b] = ds_hi8(j0 + loc, rk);
+                        const uint32_t h24 = (hi8[b] << 16) | (fmix32(colbase(j0 + loc) + rk2) >> 16);   // h >> 8
+                        hf[b] = (float)h24 * 0x1p-24f;                      // hf <= draw / 2^32 <= hfu
+                        hfu[b] = (float)(h24 + 1u) * 0x1p-24f;
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < CU; ++b) {
+                    if (e0 + (uint32_t)(b * 64) >= ncl) break;       // wave-uniform
+                    const float x = __uint_as_float(en[b].y), ax = fabsf(x);
+                    const uint32_t loc = en[b].x & 0x1FFFu;
+                    const bool inl = ax * q0 <= 1.0f - 0x1p-18f;
+                    const bool nz = vv[b] && !(x == 0.f);
+                    const bool sure = nz && inl && fmaf(ax, q1, hf[b]) >= 1.0f + 0x1p-20f;
+                    const bool drop = !nz || (inl && fmaf(ax, q0, hfu[b]) < 1.0f - 0x1p-20f);
+                    const bool amb = !sure && !drop;
+                    const uint32_t u = loc >> 11;
+                    uint32_t pin = 0;
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const uint64_t mh = __ballot(sure && u == (uint32_t)h);
+                        const uint32_t ph = __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, hs[h]));
+                        pin = u == (uint32_t)h ? ph : pin;
+                        hs[h] += (uint32_t)__popcll(mh);
+                    }
+                    if (sure && pin < (uint32_t)DS_HCAP)
+                        s16[u * DS_HCAP + pin] = (uint16_t)((loc & (HCHUNK - 1)) | ((en[b].y >> 31) << 11) | (1u << 12));
+                    const uint64_t ma = __ballot(amb);
+                    const uint32_t pa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, na));
+                    if (amb) sg[pa] = make_uint2(loc | (hi8[b] << 13), en[b].y);      // k_ds_resolve's entry
+                    na += (uint32_t)__popcll(ma);
+                }
             }
         }
         bool ovf = !fits;
@@ -628,18 +650,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
 // 64-entry batch at a time at 8 fixed points of the loop (between load issues), and item i-1's
 // fixed store sequence goes out at the end of item i.  Same entries, same lists, same bits.
 // ------------------------------------------------------------------------------------------
+#ifndef FLC_DS2_CAP
+#define FLC_DS2_CAP 384              // k_ds_filter2 staging capacity per item (4.7 %; C4 items hold ~2.3 %)
+#endif
 #ifndef FLC_DS2_WPE
-#define FLC_DS2_WPE 4                // LDS: 40 KB per block, 4 blocks per CU
+#define FLC_DS2_WPE 5                // LDS: 32 KB per block (FLC_DS2_CAP 384), 5 blocks per CU
 #endif
 template <int RING, int GCAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS2_WPE))) void k_ds_filter2(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, DsWs ws, UniformSrc) {
     constexpr int FGS = DS_FGS, NH = DS_NH;
-    static_assert(FGS == 2 && NH == 4 && GCAP == 512 && DS_HCAP == 128, "batch points / copy-out layout");
+    // GCAP: the staging capacity (candidates per item; more -> the row is folded dense), at most
+    // DS_GCAP, the stride of the items' ambiguous-entry regions
+    static_assert(FGS == 2 && NH == 4 && GCAP % 128 == 0 && GCAP <= DS_GCAP && DS_HCAP == 128, "batch points / copy-out layout");
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
     constexpr int NB = GCAP / 64;                          // classification batches of one item
     constexpr int DS_ITEM_STORES = 4 + GCAP / 128;          // partial, itm, tab, sure and ambiguous copy-outs
     __shared__ __attribute__((aligned(16))) uint2 stage[2][4][GCAP + 64];
-    __shared__ __attribute__((aligned(16))) uint16_t stage16[4][GCAP];
+    __shared__ __attribute__((aligned(16))) uint16_t stage16[4][NH * DS_HCAP];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t G = ws.G;
@@ -759,7 +786,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_DS2_WPE
         }
         {
             const uint32_t nrec = (pv && !ovf) ? ((na + 1u) & ~1u) * 8u : 0u;
-            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.enta + prow * ws.cap + pgi * GCAP, (short)0, (int)nrec, 0x00020000);
+            const auto od = __builtin_amdgcn_make_buffer_rsrc(ws.enta + prow * ws.cap + pgi * DS_GCAP, (short)0, (int)nrec, 0x00020000);
             const uint4* sq = reinterpret_cast<const uint4*>(stage[par ^ 1][wv]);
 #pragma unroll
             for (int k = 0; k < GCAP / 128; ++k) {
@@ -1399,7 +1426,7 @@ bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n,
     const int m = prm->flags & FLC_PATH_MASK;
     if (m) return m == FLC_PATH_SPARSE;
     const double share = 1.1 * (double)prm->s / sqrt((double)d) + 0.003;
-    return share * DS_FGS * CHUNK <= DS_GCAP / 1.4;
+    return share * DS_FGS * CHUNK <= (FLC_DS_V2 ? FLC_DS2_CAP : DS_GCAP) / 1.4;
 }
 
 size_t ds_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
@@ -1456,7 +1483,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
                   : v.probe == 1 ? k_ds_filter<16, DS_GCAP, 1> : v.probe == 2 ? k_ds_filter<16, DS_GCAP, 2>
                   : v.probe == 3 ? k_ds_filter<16, DS_GCAP, 3> : v.probe == 4 ? k_ds_filter<16, DS_GCAP, 4>
                   : v.probe == 5 ? k_ds_filter<16, DS_GCAP, 5> : v.probe == 6 ? k_ds_filter<16, DS_GCAP, 6>
-                  : FLC_DS_V2 ? k_ds_filter2<16, DS_GCAP> : k_ds_filter<16, DS_GCAP>;
+                  : FLC_DS_V2 ? k_ds_filter2<16, FLC_DS2_CAP> : k_ds_filter<16, DS_GCAP>;
         int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
         if (v.resident || (K > 1 && v.gridpct < 100)) {
             int per = 0, dev = 0, cus = 0;

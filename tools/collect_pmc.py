@@ -47,19 +47,21 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--kernel", default=None, help="another kernel of the workload (default: its dominant one)")
     ap.add_argument("--tag", default=None, help="output name profiles/pmc_<tag>.json (default: the workload)")
+    ap.add_argument("--compat", action="store_true", help="the compat-pattern line (resident numpy-stream patterns)")
     a = ap.parse_args()
     kernel = a.kernel or KERNEL_SUBSTR[a.workload]
-    tag = a.tag or a.workload
-    extra = ["--steps", str(a.steps), "--warmup", "1"] + (["--n", str(a.n)] if a.n else [])
+    tag = a.tag or (a.workload + ("_compat" if a.compat else ""))
+    extra = ["--steps", str(a.steps), "--warmup", "1"] + (["--n", str(a.n)] if a.n else []) + (["--compat"] if a.compat else [])
     os.environ.setdefault("TMPDIR", "/tmp")
     base = os.path.join(ROOT, "gpurun_out", f"pmc_traffic_{tag}")
     fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch", kernel)
     write, nw = run_pass("WRITE_SIZE", a.workload, extra, base + "_write", kernel)
     launches = max(nf, nw, 1)
-    res = {"workload": a.workload, "kernel": kernel, "n_override": a.n,
+    res = {"workload": a.workload, "kernel": kernel, "n_override": a.n, "compat": bool(a.compat),
            "launches": launches, "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024 / launches),
-           "correction": "2 x FETCH_SIZE (gfx950 counts half of 16 B/lane streaming reads) + WRITE_SIZE, KiB->B"}
+           "correction": "2 x FETCH_SIZE (gfx950 tallies each 128-B line request at 64 B: every streamed "
+                         "array here is read as whole lines) + WRITE_SIZE, KiB->B"}
     for d in ("profiles", "gpurun_out"):       # gpurun_out/ is what travels back from the GPU box
         os.makedirs(os.path.join(ROOT, d), exist_ok=True)
         with open(os.path.join(ROOT, d, f"pmc_{tag}.json"), "w") as f:
