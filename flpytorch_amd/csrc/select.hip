@@ -2202,6 +2202,9 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, (float*)nullptr);
 }
 
+#ifndef FLC_TK_SIDE_NT
+#define FLC_TK_SIDE_NT 256            // threads of the side-stream candidate selects (256 or 512)
+#endif
 #ifndef FLC_TK_EXACT_WG
 #define FLC_TK_EXACT_WG 256           // workgroups of the one exact-rows launch (one per CU)
 #endif
@@ -2440,6 +2443,12 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                     // few rows, or the last tail group (its select is exposed, nothing runs beside it):
                     // 1024-thread workgroups, twice the loads in flight per row
                     hipLaunchKernelGGL(k_cand_select<1024>, dim3((unsigned)rn), dim3(1024), 0, sside, r0, rn, K, ws);
+                else if (FLC_TK_SIDE_NT == 256)
+                    // beside the next group's filter: one wave per SIMD (66 VGPRs) fits in the VGPRs the
+                    // filter's three waves per SIMD leave free, so the select co-resides with the
+                    // filter's blocks instead of displacing one (512-thread selects slowed the filter
+                    // they ran beside by ~8 %, round-4 trace)
+                    hipLaunchKernelGGL(k_cand_select<256>, dim3(grid_stride_blocks(rn, 8192)), dim3(256), 0, sside, r0, rn, K, ws);
                 else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(rn, 8192)), dim3(512), 0, sside, r0, rn, K, ws); }
                 FLC_CHECK_LAUNCH("k_cand_select");
             }
