@@ -1367,6 +1367,12 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
 #ifndef FLC_DS_V2
 #define FLC_DS_V2 0                  // device-RNG filter: classification pipelined into the next item (k_ds_filter2)
 #endif
+#ifndef FLC_DS_LDSPAD
+#define FLC_DS_LDSPAD 5120           // row groups: extra LDS per filter block (bytes), room for the side tail
+#endif
+#ifndef FLC_DS_RG_SIDE
+#define FLC_DS_RG_SIDE 1             // row groups: norm + resolve on the side stream too
+#endif
 #ifndef FLC_DS_PROBE_DEF
 #define FLC_DS_PROBE_DEF 0           // A/B variant builds only (a probe's outputs are NOT valid)
 #endif
@@ -1454,11 +1460,16 @@ static int tail_groups(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, n));
 }
 
-// Row groups of the fold pipeline: the caller's hint (FLC_ROW_GROUPS(g) in flags), else 1
-// (measured: folds beside an unrestricted filter are starved, K = 2..8 no faster than 1).
+// Row groups of the pipeline: the caller's hint (FLC_ROW_GROUPS(g) in flags), else 2 for 128 rows
+// or more.  Group g's norm, resolve and fold run on the side stream under group g + 1's filter,
+// whose blocks reserve FLC_DS_LDSPAD bytes more LDS (5 instead of 6 per CU) so that the tail
+// kernels find room beside them: C4 9.684 -> 9.554 ms per step, same allocation, two processes
+// (round 4, profiles/r04); 3 groups ran 9.89 (one more filter launch boundary), and without the
+// pad 2 groups ran 9.650 (round 3's version, the norm and resolve between the filters and no pad,
+// was not faster than 1 group).
 static int ds_groups(const flc_codec_params* prm, int64_t n) {
     const int g = (prm->flags >> 8) & 0xFF;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(g ? g : 1, n));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g ? g : (n >= 128 ? 2 : 1), n));
 }
 
 int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int64_t n, int64_t d, const float* w,
@@ -1492,8 +1503,12 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) == hipSuccess && per > 0)
                 gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
         }
+        // row groups (s2: the group's tail runs beside the next group's filter): the filter's
+        // blocks reserve FLC_DS_LDSPAD more bytes of LDS, so one block fewer fits a CU and the
+        // side stream's tail kernels find room without waiting for a filter block to retire
+        const size_t pad = s2 ? (size_t)FLC_DS_LDSPAD : 0u;
         { ProfScope _ps("k_ds_filter", st);
-        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), 0, st, rows, n, r0, rn, std::min<int64_t>(v.rb, rn), d, ws, us); }
+        hipLaunchKernelGGL(kern, dim3(gw), dim3(256), pad, st, rows, n, r0, rn, std::min<int64_t>(v.rb, rn), d, ws, us); }
         FLC_CHECK_LAUNCH("k_ds_filter");
         hipStream_t sr = st;
         if (s2) {
@@ -1564,10 +1579,20 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     }
     for (int g = 0; g < K; ++g) {
         const int64_t r0 = n * g / K, r1 = n * (g + 1) / K;
-        int rc = filter(r0, r1 - r0);
+        int rc;
+        if (FLC_DS_RG_SIDE) {
+            // the group's whole tail (norm, resolve, fold) on the side stream, under the next
+            // group's filter
+            filt_ev = cx.ev[g];
+            rc = filter(r0, r1 - r0, cx.side);
+        } else {
+            rc = filter(r0, r1 - r0);
+            if (!rc) {
+                FLC_CHECK_HIP(hipEventRecord(cx.ev[g], st));
+                FLC_CHECK_HIP(hipStreamWaitEvent(cx.side, cx.ev[g], 0));
+            }
+        }
         if (rc) return rc;
-        FLC_CHECK_HIP(hipEventRecord(cx.ev[g], st));
-        FLC_CHECK_HIP(hipStreamWaitEvent(cx.side, cx.ev[g], 0));
         rc = accum(r0, r1 - r0, g == 0, g == K - 1, cx.side);
         if (rc) return rc;
     }

@@ -65,6 +65,7 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* carrive;    // [N * RCS] its per-row arrival counters
     uint32_t* shcnt;      // [N][CS_SH * RCS] few rows: the filter's reservation counters, one per shard
     uint32_t* zm;         // [C][CHUNK / 32] k_chunk_accum (one-wave blocks): a fold job's kept-column mask
+    float* part;          // [D] TopK row-group folds: the running tiles carried from one group to the next
     int64_t cap;
 };
 
@@ -276,15 +277,13 @@ __device__ inline float4 cs_ld(const float4* p) {
 #endif
 }
 template <int NT>
-__global__ __launch_bounds__(NT) void k_cand_select(int64_t r0, int64_t rn, int64_t K, SelWs ws) {
-    __shared__ uint32_t h[HBINS];
-    __shared__ uint32_t scratch[260];
-    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
-        if (ws.flags[row]) continue;                                     // overflowed in the filter
+__device__ void cand_select_row(int64_t row, int64_t K, SelWs ws, uint32_t* h, uint32_t* scratch) {
+    {
+        if (ws.flags[row]) return;                                       // overflowed in the filter
         const uint32_t cnt = ws.rowcnt[(row) * RCS];
         if (cnt < (uint32_t)K) {                                          // sample threshold too high
             if (threadIdx.x == 0) ws.flags[row] |= F_SHORT;
-            continue;
+            return;
         }
         const uint32_t T = ws.thr[row];
         const uint32_t span = ws.prefix[row] - T;                         // kest >= T
@@ -372,6 +371,16 @@ __global__ __launch_bounds__(NT) void k_cand_select(int64_t r0, int64_t rn, int6
                 if (ties) ws.flags[row] |= F_TIES;
             }
         }
+        __syncthreads();
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_cand_select(int64_t r0, int64_t rn, int64_t K, SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
+        cand_select_row<NT>(row, K, ws, h, scratch);
         __syncthreads();
     }
 }
@@ -997,7 +1006,8 @@ constexpr int EX_NT = 1024;
 constexpr int EX_U = 8;                      // float4 loads per thread in flight in the radix passes
 
 // exclusive prefix of v over the workgroup's threads (in thread order) and the total
-__device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [EX_NT / 64] */, uint32_t& total) {
+template <int NT = EX_NT>
+__device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [NT / 64] */, uint32_t& total) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t inc = v;
 #pragma unroll
@@ -1009,7 +1019,7 @@ __device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [EX_NT / 64
     __syncthreads();
     uint32_t before = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < EX_NT / 64; ++k) {
+    for (int k = 0; k < NT / 64; ++k) {
         const uint32_t x = wsum[k];
         before += k < wv ? x : 0u;
         tot += x;
@@ -1021,7 +1031,7 @@ __device__ inline uint32_t ex_scan(uint32_t v, uint32_t* wsum /* LDS [EX_NT / 64
 
 // One row's exact selection by one EX_NT-thread workgroup: three radix passes over the row, then the
 // row's list rewritten with exactly its admitted entries in index order (ties: the lowest indices).
-template <bool VEC>
+template <bool VEC, int NT = EX_NT>
 __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_t K, SelWs ws, uint32_t* h,
                           uint32_t* scratch, uint32_t* wsum) {
     const int t = threadIdx.x;
@@ -1030,7 +1040,7 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
         const float* r = rows.row(row);
         uint32_t prefix = 0, krem = (uint32_t)K;
         for (int p = 0; p < 3; ++p) {
-            for (int i = t; i < HBINS; i += EX_NT) h[i] = 0;
+            for (int i = t; i < HBINS; i += NT) h[i] = 0;
             __syncthreads();
             auto add = [&](uint32_t k) { if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u); };
             int64_t j = 0;
@@ -1038,22 +1048,22 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
                 const float4* r4 = reinterpret_cast<const float4*>(r);
                 const int64_t g4 = d / 4;
                 int64_t g = t;
-                for (; g + (EX_U - 1) * EX_NT < g4; g += EX_U * EX_NT) {
+                for (; g + (EX_U - 1) * NT < g4; g += EX_U * NT) {
                     float4 q[EX_U];
 #pragma unroll
-                    for (int u = 0; u < EX_U; ++u) q[u] = ld_row4(r4 + g + u * EX_NT);
+                    for (int u = 0; u < EX_U; ++u) q[u] = ld_row4(r4 + g + u * NT);
 #pragma unroll
                     for (int u = 0; u < EX_U; ++u) {
                         add(mag_key(q[u].x)); add(mag_key(q[u].y)); add(mag_key(q[u].z)); add(mag_key(q[u].w));
                     }
                 }
-                for (; g < g4; g += EX_NT) {
+                for (; g < g4; g += NT) {
                     const float4 q = ld_row4(r4 + g);
                     add(mag_key(q.x)); add(mag_key(q.y)); add(mag_key(q.z)); add(mag_key(q.w));
                 }
                 j = g4 * 4;
             }
-            for (int64_t jj = j + t; jj < d; jj += EX_NT) add(mag_key(r[jj]));
+            for (int64_t jj = j + t; jj < d; jj += NT) add(mag_key(r[jj]));
             __syncthreads();
             uint32_t bin, above;
             hist_find(h, krem, bin, above, scratch);
@@ -1086,7 +1096,7 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
                 ne += eq[q] ? 1u : 0u;
             }
             uint32_t etot;
-            uint32_t erank = tie_run + ex_scan(ne, wsum, etot);        // ties before this thread's
+            uint32_t erank = tie_run + ex_scan<NT>(ne, wsum, etot);        // ties before this thread's
             uint32_t na = 0;
             bool adm[4];
 #pragma unroll
@@ -1096,7 +1106,7 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
                 na += adm[q] ? 1u : 0u;
             }
             uint32_t atot;
-            uint32_t pos = base + ex_scan(na, wsum, atot);
+            uint32_t pos = base + ex_scan<NT>(na, wsum, atot);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if (adm[q]) { oi[pos] = (uint32_t)(j0 + q); ov[pos] = v[q]; ++pos; }
@@ -1123,6 +1133,28 @@ __global__ __launch_bounds__(EX_NT) void k_topk_exact_rows(RowSrc rows, int64_t 
     for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
         if (!(ws.flags[row] & (F_OVERFLOW | F_SHORT))) continue;       // row-uniform
         exact_row<VEC>(rows, n, row, d, K, ws, h, scratch, wsum);
+    }
+}
+
+// The many-row candidate select with the exact fallback in the same workgroup: a row whose list
+// overflowed in the filter, came up short, or whose K-th key the digits could not settle is
+// selected exactly right here (exact_row with this workgroup's NT threads), so the group's
+// select leaves every row final and no separate exact launch (a grid of 1024-thread workgroups
+// that waited for whole CUs beside the next filter) follows it.
+template <int NT, bool VEC>
+__global__ __launch_bounds__(NT) void k_cand_select_x(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, int64_t K,
+                                                      SelWs ws) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t wsum[NT / 64];
+    __shared__ uint32_t failed;
+    for (int64_t row = r0 + blockIdx.x; row < r0 + rn; row += gridDim.x) {
+        cand_select_row<NT>(row, K, ws, h, scratch);
+        __syncthreads();
+        if (threadIdx.x == 0) failed = __atomic_load_n(&ws.flags[row], __ATOMIC_RELAXED) & (F_OVERFLOW | F_SHORT);
+        __syncthreads();
+        if (failed) exact_row<VEC, NT>(rows, n, row, d, K, ws, h, scratch, wsum);
+        __syncthreads();
     }
 }
 
@@ -1418,6 +1450,12 @@ __global__ __launch_bounds__(RK_FTHR) void k_randk_fine(RowSrc rows, int64_t n, 
 // flight while a row is folded (a ring of AP register slots, 2 x 64 entries per row), so the
 // wave never waits on a dependent tab -> entries round trip.
 // ------------------------------------------------------------------------------------------
+#ifndef FLC_CA_PROBE
+#define FLC_CA_PROBE 0               // A/B cost probe of k_chunk_accum (outputs NOT valid): 1 no tile update
+#endif
+#ifndef FLC_CA_AP1
+#define FLC_CA_AP1 4                 // one-wave fold workgroups: rows in flight (<= 113 VGPRs: beside the TopK filter's 3 waves per SIMD)
+#endif
 #ifndef FLC_CA_WPB1
 #define FLC_CA_WPB1 0                // k_chunk_accum over whole chunks: one-wave workgroups
 #endif
@@ -1432,11 +1470,11 @@ struct RowMeta {
     float w;
 };
 
-__device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64_t r, const float* w) {
+__device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64_t r, const float* w, int64_t rend = -1) {
     RowMeta m;
     m.te = make_uint2(0, 0);
     m.thr = 0; m.cut = 0xFFFFFFFFu; m.mode = 0; m.w = 1.f;
-    if (r < n) {
+    if (r < (rend < 0 ? n : rend)) {
         m.te = ws.tab[c * n + r];
         m.thr = ws.thr[r];
         const uint32_t f = ws.flags[r];
@@ -1578,23 +1616,27 @@ __device__ void resolve_neg_zero_g(float* tl, uint32_t* rm, const SelWs& ws, int
 // 160 KB and every chunk of a 10 M row (2442) has its wave resident at once — with 4-wave blocks
 // (67.5 KB with the masks) two fit a CU, 2048 chunk waves ran and the last 394 formed a second
 // round of the same length.
-template <bool ASSIGN, int TS = CHUNK, bool W = true, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WPB == 1 ? 3 : 1))) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w,
-                                                          float wt, float* __restrict__ out) {
+// Row groups: rows [r0, rend) only; `first` starts the tiles at -0, else from ws.part (the previous
+// group's tiles); `last` resolves the -0 columns over ALL n rows and writes out = sums / wt, else
+// the tiles go back to ws.part.  (r0 = 0, rend = n, first = last = 1: one fold of every row.)
+template <bool ASSIGN, int TS, bool W, int WPB, int AP = AP>
+__device__ __forceinline__ void chunk_accum_body(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w, float wt,
+                                                 float* __restrict__ out, int64_t r0, int64_t rend, int first, int last,
+                                                 float (*tile)[TS], uint32_t (*zmask)[WPB == 1 ? 1 : TS / 32]) {
+    if (rend < 0) rend = n;
     constexpr int PARTS = CHUNK / TS;
-    __shared__ __attribute__((aligned(16))) float tile[WPB][TS];
-    __shared__ uint32_t zmask[WPB == 1 ? 1 : WPB][WPB == 1 ? 1 : TS / 32];
     const int lane = threadIdx.x & 63;
     const int wv = WPB == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t C = nchunks(d);
     float* tl = tile[wv];
-    const int64_t nb = (n + 63) / 64;                  // row batches
+    const int64_t nb = (rend - r0 + 63) / 64;          // row batches
     for (int64_t t = (int64_t)blockIdx.x * WPB + wv; t < C * PARTS; t += (int64_t)gridDim.x * WPB) {
         const int64_t c = t / PARTS;
-        // ASSIGN (compressVector: out = zeros, out[kept] = x) stores into +0; the fold adds into -0
-        for (int i = lane; i < TS; i += 64) tl[i] = ASSIGN ? 0.f : -0.f;
         const uint32_t cbase = (uint32_t)(c * CHUNK + (t % PARTS) * TS);
-        RowMeta cur = load_meta(ws, c, n, lane, w), nxt;
+        // ASSIGN (compressVector: out = zeros, out[kept] = x) stores into +0; the fold adds into -0
+        for (int i = lane; i < TS; i += 64)
+            tl[i] = ASSIGN ? 0.f : (first || (int64_t)cbase + i >= d ? -0.f : ws.part[cbase + i]);
+        RowMeta cur = load_meta(ws, c, n, r0 + lane, w, rend), nxt;
         // ring of AP rows' entries (the first 128 of each list; range-checked buffer loads, lanes
         // past the list end get index ~0 = no column)
         uint32_t ri[AP][2];
@@ -1618,16 +1660,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WPB ==
             const uint32_t loc = ix - cbase;                   // ~0 index / other part: loc >= TS
             const uint64_t a = ((uint64_t)mag_key(vv) << 32) | (uint64_t)(~ix);
             const uint64_t b = ((uint64_t)T << 32) | (uint64_t)(~cut);
+            if (FLC_CA_PROBE == 1) {                          // cost probe: no tile update
+                if (loc < (uint32_t)TS && a >= b && vv == 1.2345f) tl[0] = vv;
+                return;
+            }
             if (loc < (uint32_t)TS && a >= b) {
                 if (ASSIGN) tl[loc] = vv;
                 else tl[loc] = W ? tl[loc] + wi * vv : tl[loc] + vv;
             }
         };
 #pragma unroll
-        for (int q = 0; q < AP; ++q) fetch(cur, q, q, q);
+        for (int q = 0; q < AP; ++q) fetch(cur, q, r0 + q, q);
         for (int64_t b = 0; b < nb; ++b) {
-            const int64_t i0 = b * 64;
-            nxt = load_meta(ws, c, n, i0 + 64 + lane, w);    // next batch's state, one batch ahead
+            const int64_t i0 = r0 + b * 64;
+            nxt = load_meta(ws, c, n, i0 + 64 + lane, w, rend);   // next batch's state, one batch ahead
             if (__builtin_expect(__ballot(cur.te.y > 128u) == 0ull, 1)) {
                 // every list of the batch fits the ring slots: straight-line pipeline
 #pragma unroll
@@ -1682,12 +1728,38 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WPB ==
             cur = nxt;
         }
         const int64_t len = min((int64_t)TS, d - (int64_t)cbase);
+        if (!last) {                                   // row groups: the tiles carry on to the next group
+            for (int64_t i = lane; i < len; i += 64) ws.part[cbase + i] = tl[i];
+            continue;
+        }
         if (!ASSIGN) {
             if (WPB == 1) resolve_neg_zero_g<TS>(tl, ws.zm + t * (TS / 32), ws, c, n, cbase, len, w, lane);
             else resolve_neg_zero<TS>(tl, zmask[wv], ws, c, n, cbase, len, w, lane);
         }
         for (int64_t i = lane; i < len; i += 64) out[cbase + i] = ASSIGN ? tl[i] : tl[i] / wt;
     }
+}
+
+template <bool ASSIGN, int TS = CHUNK, bool W = true>
+__global__ __launch_bounds__(256) void k_chunk_accum(int64_t n, int64_t d, SelWs ws, const float* __restrict__ w, float wt,
+                                                     float* __restrict__ out, int64_t r0 = 0, int64_t rend = -1,
+                                                     int first = 1, int last = 1) {
+    __shared__ __attribute__((aligned(16))) float tile[4][TS];
+    __shared__ uint32_t zmask[4][TS / 32];
+    chunk_accum_body<ASSIGN, TS, W, 4>(n, d, ws, w, wt, out, r0, rend, first, last, tile, zmask);
+}
+
+// one-wave workgroups holding only their tile (16 KB) and at most FLC_CA_VGPR1 VGPRs: they fit in
+// what the TopK filter's waves leave free on a CU (row-group folds under the next group's filter)
+// (the tile is dynamic LDS, CHUNK floats given at launch: with a static 16 KB array the compiler
+// takes LDS as the occupancy limit and ignores the waves-per-EU request)
+template <bool W>
+__global__ __launch_bounds__(64) void k_chunk_accum1(
+        int64_t n, int64_t d, SelWs ws, const float* __restrict__ w, float wt, float* __restrict__ out, int64_t r0,
+        int64_t rend, int first, int last) {
+    extern __shared__ __attribute__((aligned(16))) float dyn_tile[];
+    chunk_accum_body<false, CHUNK, W, 1, FLC_CA_AP1>(n, d, ws, w, wt, out, r0, rend, first, last,
+                                         reinterpret_cast<float (*)[CHUNK]>(dyn_tile), nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2117,6 +2189,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     s.worklist = cv.take<uint32_t>(nn);
     s.nwork = cv.take<uint32_t>(4);
     s.zm = cv.take<uint32_t>((size_t)C * (CHUNK / 32));
+    s.part = codec == FLC_TOPK ? cv.take<float>((size_t)C * CHUNK) : nullptr;
     if (codec == FLC_TOPK) {
         s.tieprefix = cv.take<uint32_t>((size_t)C * nn);
         s.tiecut = cv.take<uint32_t>(nn);
@@ -2202,8 +2275,11 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, (float*)nullptr);
 }
 
+#ifndef FLC_TK_GFOLD
+#define FLC_TK_GFOLD 1                // many-row TopK: fold each row group under the next group's filter
+#endif
 #ifndef FLC_TK_SIDE_NT
-#define FLC_TK_SIDE_NT 256            // threads of the side-stream candidate selects (256 or 512)
+#define FLC_TK_SIDE_NT 512            // threads of the side-stream candidate selects (256 or 512)
 #endif
 #ifndef FLC_TK_EXACT_WG
 #define FLC_TK_EXACT_WG 256           // workgroups of the one exact-rows launch (one per CU)
@@ -2318,6 +2394,30 @@ int randk_device_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc
     return launch_chunk_accum(n, d, sw, false, w, wt, out, st);
 }
 
+// TopK row-group fold: rows [r0, r1) into the running tiles (ws.part); beside a filter the
+// one-wave workgroups (<= 102 VGPRs, 16 KB of LDS: room is left beside the filter's waves), the
+// exposed last group in 4-wave workgroups
+static int launch_group_fold(int64_t n, int64_t d, SelWs ws, const float* w, float wt, float* out, int64_t r0, int64_t r1,
+                             bool first, bool last, bool exposed, hipStream_t st) {
+    const int64_t C = host_chunks(d);
+    ProfScope _ps("k_chunk_accum", st);
+    if (!exposed) {
+        const int ab = grid_stride_blocks(C, 16384);
+        if (w) hipLaunchKernelGGL((k_chunk_accum1<true>), dim3(ab), dim3(64), CHUNK * sizeof(float), st, n, d, ws, w, wt, out, r0, r1,
+                                  first ? 1 : 0, last ? 1 : 0);
+        else hipLaunchKernelGGL((k_chunk_accum1<false>), dim3(ab), dim3(64), CHUNK * sizeof(float), st, n, d, ws, w, wt, out, r0, r1,
+                                first ? 1 : 0, last ? 1 : 0);
+    } else {
+        const int ab = grid_stride_blocks((C + 3) / 4, 4096);
+        if (w) hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out, r0, r1,
+                                  first ? 1 : 0, last ? 1 : 0);
+        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out, r0, r1,
+                                first ? 1 : 0, last ? 1 : 0);
+    }
+    FLC_CHECK_LAUNCH("k_chunk_accum(group)");
+    return FLC_OK;
+}
+
 // chunk-owner fold of the rows' lists (TopK candidates, RandK members)
 static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const float* w, float wt, float* out,
                               hipStream_t st) {
@@ -2338,8 +2438,8 @@ static int launch_chunk_accum(int64_t n, int64_t d, SelWs ws, bool assign, const
     else if (FLC_CA_WPB1 && !assign) {
         // one-wave workgroups (the tile alone in LDS), one per chunk
         const int ab = grid_stride_blocks(C, 16384);
-        if (w) hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, true, 1>), dim3(ab), dim3(64), 0, st, n, d, ws, w, wt, out);
-        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, false, 1>), dim3(ab), dim3(64), 0, st, n, d, ws, w, wt, out);
+        if (w) hipLaunchKernelGGL((k_chunk_accum1<true>), dim3(ab), dim3(64), CHUNK * sizeof(float), st, n, d, ws, w, wt, out, (int64_t)0, n, 1, 1);
+        else hipLaunchKernelGGL((k_chunk_accum1<false>), dim3(ab), dim3(64), CHUNK * sizeof(float), st, n, d, ws, w, wt, out, (int64_t)0, n, 1, 1);
     } else go(std::integral_constant<int, CHUNK>{}, grid_stride_blocks((C + 3) / 4, 4096));
     }
     FLC_CHECK_LAUNCH("k_chunk_accum");
@@ -2361,7 +2461,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (ws_bytes < need) { set_error("select: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
     SelWs ws = carve_sel(wsp, codec, n, d, K, nullptr);
     const int64_t C = host_chunks(d);
-    bool lone_assign = false;
+    bool lone_assign = false, gfold = false;
     // TopK, few rows: sharded candidate lists (k_topk_filter_fast) and the spread select (k_cs_pass)
     const bool few = codec == FLC_TOPK && n <= CS_FEW && !cs_single() && sel_capacity(codec, d, K) >= (int64_t)CS_SH * GCAP;
     if (codec == FLC_RANDK) {
@@ -2398,6 +2498,9 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             // fallback of the group's rows; with TG > 1 groups the select + fallback of group g run
             // on a side stream under the filter of group g + 1 (both per-row, other rows' lists)
             const int TG = few ? 1 : tk_tail_groups(n);
+            // many rows: each group's select does its own exact fallback and its rows are folded
+            // right after it (tiles carried in ws.part), under the next group's filter
+            gfold = FLC_TK_GFOLD && !few && !assign && !dense_k;
             hipStream_t sside = st;
             TkCtx* cx = nullptr;
             std::unique_lock<std::mutex> lk;
@@ -2439,6 +2542,23 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 if (few) {
                     for (int p = 0; p < 3; ++p)
                         hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws);
+                } else if (gfold) {
+                    // the select with the exact fallback in the same workgroup (every row final after
+                    // it), then the group's rows folded into the running tiles, both on the side stream
+                    // under the next group's filter (the last group's: exposed)
+                    const bool big = rn < 128 || g == TG - 1;
+                    const int nt = big ? 1024 : FLC_TK_SIDE_NT;
+                    const dim3 grid((unsigned)(big ? rn : grid_stride_blocks(rn, 8192)));
+                    if (big) {
+                        if (vec) hipLaunchKernelGGL((k_cand_select_x<1024, true>), grid, dim3(nt), 0, sside, rows, n, r0, rn, d, K, ws);
+                        else hipLaunchKernelGGL((k_cand_select_x<1024, false>), grid, dim3(nt), 0, sside, rows, n, r0, rn, d, K, ws);
+                    } else if (FLC_TK_SIDE_NT == 256) {
+                        if (vec) hipLaunchKernelGGL((k_cand_select_x<256, true>), grid, dim3(nt), 0, sside, rows, n, r0, rn, d, K, ws);
+                        else hipLaunchKernelGGL((k_cand_select_x<256, false>), grid, dim3(nt), 0, sside, rows, n, r0, rn, d, K, ws);
+                    } else {
+                        if (vec) hipLaunchKernelGGL((k_cand_select_x<512, true>), grid, dim3(nt), 0, sside, rows, n, r0, rn, d, K, ws);
+                        else hipLaunchKernelGGL((k_cand_select_x<512, false>), grid, dim3(nt), 0, sside, rows, n, r0, rn, d, K, ws);
+                    }
                 } else if (rn < 128 || (TG > 1 && g == TG - 1))
                     // few rows, or the last tail group (its select is exposed, nothing runs beside it):
                     // 1024-thread workgroups, twice the loads in flight per row
@@ -2451,8 +2571,13 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                     hipLaunchKernelGGL(k_cand_select<256>, dim3(grid_stride_blocks(rn, 8192)), dim3(256), 0, sside, r0, rn, K, ws);
                 else hipLaunchKernelGGL(k_cand_select<512>, dim3(grid_stride_blocks(rn, 8192)), dim3(512), 0, sside, r0, rn, K, ws); }
                 FLC_CHECK_LAUNCH("k_cand_select");
+                if (gfold) {
+                    const bool lastg = g == TG - 1;
+                    if (int rc = launch_group_fold(n, d, ws, w, wt, out, r0, r0 + rn, g == 0, lastg, lastg || TG == 1, sside))
+                        return rc;
+                }
             }
-            if (!lone_assign) {
+            if (!lone_assign && !gfold) {
                 // rows the fast path failed (rare): exact selection of every group's failed rows in
                 // ONE launch after the last group's select (a workgroup per row, grid-stride, rows
                 // that did not fail return at once).  Per-group launches beside the next group's
@@ -2504,6 +2629,7 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
         FLC_CHECK_LAUNCH("k_assign_finish");
         return FLC_OK;
     }
+    if (gfold) return FLC_OK;                       // the last group's fold wrote out
     if (assign && n == 1 && codec == FLC_TOPK && !assign_fold()) {
         FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)d * sizeof(float), st));
         const int sb = (int)std::max<int64_t>(1, std::min<int64_t>((sel_capacity(codec, d, K) + 255) / 256, 2048));

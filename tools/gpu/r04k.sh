@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4: (1) TopK side selects 256 vs 512 threads; chunk-fold probe; (2) QSGD row groups with the
+# whole tail on the side stream, with and without an LDS pad that leaves room beside the filter
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+out=gpurun_out/${1:-r04k}; mkdir -p $out
+T="python -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread"
+timeout -k 10 400 $T tests/test_gpu_parity.py tests/test_gpu_dither_sparse.py -k "topk or row_groups" > $out/tests.log 2>&1 || exit $?
+A="python tools/ab_inproc.py --rounds 4 --steps 5 --prof-modes off"
+timeout -k 10 400 $A --workload c3 --variants prod,s512 > $out/ab_c3_a.txt 2>&1 || exit $?
+timeout -k 10 400 $A --workload c4 --variants prod,prod:rg2,prod:rg4,pad5k:rg2,pad5k:rg4 --rounds 3 > $out/ab_c4_rg.txt 2>&1 || exit $?
+timeout -k 10 400 $A --workload c3 --variants s512,prod > $out/ab_c3_b.txt 2>&1 || exit $?
+timeout -k 10 400 python tools/ab_inproc.py --rounds 3 --steps 5 --no-bitcheck --workload c3 --variants prod,fp1 > $out/ab_c3_fp.txt 2>&1 || exit $?
+exit 0
