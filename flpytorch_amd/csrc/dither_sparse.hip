@@ -1370,6 +1370,9 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
 #ifndef FLC_DS_LDSPAD
 #define FLC_DS_LDSPAD 5120           // row groups: extra LDS per filter block (bytes), room for the side tail
 #endif
+#ifndef FLC_DS_LASTPCT
+#define FLC_DS_LASTPCT 100           // size of the last QSGD row group in % of the others (its tail is exposed)
+#endif
 #ifndef FLC_DS_RG_SIDE
 #define FLC_DS_RG_SIDE 1             // row groups: norm + resolve on the side stream too
 #endif
@@ -1578,7 +1581,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         return accum(0, n, 1, 1, st);
     }
     for (int g = 0; g < K; ++g) {
-        const int64_t r0 = n * g / K, r1 = n * (g + 1) / K;
+        const int64_t r0 = group_row(n, K, g, FLC_DS_LASTPCT), r1 = group_row(n, K, g + 1, FLC_DS_LASTPCT);
         int rc;
         if (FLC_DS_RG_SIDE) {
             // the group's whole tail (norm, resolve, fold) on the side stream, under the next

@@ -2275,6 +2275,9 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, (float*)nullptr);
 }
 
+#ifndef FLC_TK_LASTPCT
+#define FLC_TK_LASTPCT 100            // size of the last TopK row group in % of the others (its tail is exposed)
+#endif
 #ifndef FLC_TK_GFOLD
 #define FLC_TK_GFOLD 1                // many-row TopK: fold each row group under the next group's filter
 #endif
@@ -2522,7 +2525,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 sside = cx->side;
             }
             for (int g = 0; g < TG; ++g) {
-                const int64_t r0 = n * g / TG, rn = n * (g + 1) / TG - r0;
+                const int64_t r0 = group_row(n, TG, g, FLC_TK_LASTPCT), rn = group_row(n, TG, g + 1, FLC_TK_LASTPCT) - r0;
                 { ProfScope _ps("k_topk_filter", st);
                 // few rows: 2-chunk groups (twice the waves in flight for a lone row)
                 // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
