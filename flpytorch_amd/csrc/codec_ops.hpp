@@ -202,9 +202,10 @@ struct DitherOp {
     }
     // NE elements, written stage by stage (each step for all elements before the next) so the NE
     // dependency chains are interleaved in the instruction stream; one fix-up branch at the end.
+    // uv (compat only, optional): the elements' float64 draws, loaded by the caller ahead of time
     template <bool F, int NE>
     __device__ inline void apply_block(const float* x, const int64_t* jv, const uint32_t* cs, const float4* tab,
-                                       float* out) const {
+                                       float* out, const double* uv = nullptr) const {
         float y[NE], p2[NE];
         float4 t[NE];
         bool fix[NE];
@@ -230,7 +231,8 @@ struct DitherOp {
         for (int c = 0; c < NE / 4; ++c) hg[c] = hg_of<COMPAT>(rk, jv[4 * c]);
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
-            const bool down = draw_below<COMPAT>(urow, rk, jv[e], cs[e], hg[e / 4], COMPAT ? ldexpf(p2[e], -32) : 0.f, p2[e]);
+            const bool down = (COMPAT && uv) ? uv[e] < (double)ldexpf(p2[e], -32)
+                                             : draw_below<COMPAT>(urow, rk, jv[e], cs[e], hg[e / 4], COMPAT ? ldexpf(p2[e], -32) : 0.f, p2[e]);
             const float lev = down ? t[e].x : t[e].y;
             out[e] = (x[e] == 0.f) ? 0.f : copysignf(lev, x[e]) * dn.b;
             any |= fix[e];

@@ -17,6 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "codec_ops.hpp"
 #include "wire_codes.hpp"
 
@@ -52,7 +54,7 @@ __device__ inline double ncomb(double a, double b) {
 __device__ inline uint32_t is_tiny(float v) { const float a = fabsf(v); return (a != 0.f && a < 0x1p-80f) ? 1u : 0u; }
 
 // DIFF: the row is the fp32 difference src.row(0) - sub (the shift codecs' C(a - b), one row)
-template <int NORM, bool VEC, bool DIFF>
+template <int NORM, bool VEC, bool DIFF, bool KEEP = false>
 __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, const float* __restrict__ sub, int64_t d,
                                                        int64_t parts, int64_t plen, double* __restrict__ partial,
                                                        uint32_t* __restrict__ tinyp) {
@@ -68,7 +70,22 @@ __global__ __launch_bounds__(256) void k_norm_partials(RowSrc src, const float* 
         uint32_t tiny = 0;
         if (VEC) {
             const int64_t g0 = j0 / 4, g1 = j1 / 4;   // j0 % 4 == 0 (plen % 4 == 0)
-            for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
+            int64_t g = g0 + threadIdx.x;
+            if (!DIFF) {
+                // 8 loads in flight per thread, accumulated in the same order as one at a time
+                for (; g + 7 * 256 < g1; g += 8 * 256) {
+                    float4 q[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        q[u] = KEEP ? reinterpret_cast<const float4*>(r)[g + u * 256] : ld_row4(reinterpret_cast<const float4*>(r) + g + u * 256);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        a = nacc<NORM>(a, q[u].x); a = nacc<NORM>(a, q[u].y); a = nacc<NORM>(a, q[u].z); a = nacc<NORM>(a, q[u].w);
+                        tiny |= is_tiny(q[u].x) | is_tiny(q[u].y) | is_tiny(q[u].z) | is_tiny(q[u].w);
+                    }
+                }
+            }
+            for (; g < g1; g += 256) {
                 float4 v = ld_row4(reinterpret_cast<const float4*>(r) + g);
                 if (DIFF) {
                     const float4 u = reinterpret_cast<const float4*>(sub)[g];
@@ -196,6 +213,117 @@ __global__ __launch_bounds__(256) void k_ew_dense(const float* __restrict__ x, i
     }
     for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += stride)
         out[j] = op.template apply<false>(x[j], j, op.col(j), smem_tab);
+}
+
+// ------------------------------------------------------------------------------------------
+// A lone row's standard dithering (compressVector, own norm): after the norm partials, ONE launch
+// in which every workgroup folds the partials itself (fixed order: the same norm in every block)
+// and encodes U float4 groups per thread per trip with all their loads — the row's and, in compat
+// mode, the float64 draws' — issued before the arithmetic.  Replaces k_norm_final + k_ew_dense
+// (one launch boundary less; the grid-stride loop of k_ew_dense kept one load per thread in flight).
+// ------------------------------------------------------------------------------------------
+constexpr int64_t LONE_PLEN = 32768;          // elements per norm partial of a lone row
+#ifndef FLC_LONE_U
+#define FLC_LONE_U 4
+#endif
+// The norm pass reads the row with ordinary loads, so the encode's second read of it finds it in
+// the caches (the 100 MB row of C4 fits the 256 MB infinity cache), and the encode's output goes
+// out with nontemporal stores: 93.5 -> 87.7 us per call at D = 25 M in compat mode (same box,
+// interleaved runs; each alone: 90.7 / 93.3 us; 8 groups per trip: 95.7 us), profiles/r04/lone_ab.txt
+#ifndef FLC_LONE_KEEP
+#define FLC_LONE_KEEP 1
+#endif
+#ifndef FLC_LONE_OUT_NT
+#define FLC_LONE_OUT_NT 1
+#endif
+constexpr int LONE_U = FLC_LONE_U;            // float4 groups per thread per trip
+
+template <int NORM, bool COMPAT, bool F>
+__device__ inline void lone_dither_body(const DitherOp<false, COMPAT>& op, const float* __restrict__ x, int64_t d,
+                                        const float4* tab, float* __restrict__ out) {
+    const int64_t n4 = d / 4;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    for (int64_t b = (int64_t)blockIdx.x * 256 * LONE_U; b < n4; b += (int64_t)gridDim.x * 256 * LONE_U) {
+        float4 v[LONE_U];
+        double uu[LONE_U][4];
+#pragma unroll
+        for (int u = 0; u < LONE_U; ++u) {
+            const int64_t g = b + u * 256 + threadIdx.x;
+            const bool in = g < n4;
+            v[u] = in ? (FLC_LONE_KEEP ? x4[g] : ld_row4(x4 + g)) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (COMPAT) {
+                const v2d* up = reinterpret_cast<const v2d*>(op.urow + 4 * g);
+                const v2d a = in ? __builtin_nontemporal_load(up) : v2d{0.0, 0.0};
+                const v2d c = in ? __builtin_nontemporal_load(up + 1) : v2d{0.0, 0.0};
+                uu[u][0] = a.x; uu[u][1] = a.y; uu[u][2] = c.x; uu[u][3] = c.y;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < LONE_U; ++u) {
+            const int64_t g = b + u * 256 + threadIdx.x;
+            if (g >= n4) continue;
+            const float xe[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            const int64_t jv[4] = {g * 4, g * 4 + 1, g * 4 + 2, g * 4 + 3};
+            uint32_t cs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cs[q] = op.col(g * 4 + q);
+            float o[4];
+            op.template apply_block<F, 4>(xe, jv, cs, tab, o, COMPAT ? uu[u] : nullptr);
+            if (FLC_LONE_OUT_NT) {
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4f{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4f*>(out) + g);
+            } else {
+                reinterpret_cast<float4*>(out)[g] = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        }
+    }
+    for (int64_t j = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; j < d; j += (int64_t)gridDim.x * 256)
+        out[j] = op.template apply<false>(x[j], j, op.col(j), tab);
+}
+
+template <int NORM, bool COMPAT>
+__global__ __launch_bounds__(256) void k_lone_dither(const float* __restrict__ x, int64_t d, DitherOp<false, COMPAT> op,
+                                                     const float* __restrict__ levels, int s, float* __restrict__ out,
+                                                     const double* __restrict__ partial, const uint32_t* __restrict__ tinyp,
+                                                     int64_t parts, float* __restrict__ pn, float* __restrict__ rpn,
+                                                     uint32_t* __restrict__ rowfast, uint64_t seed, int64_t client0,
+                                                     uint32_t* __restrict__ rk, float* __restrict__ pout) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem_tab[];
+    __shared__ double red[4];
+    __shared__ uint32_t redt[4];
+    const bool tab_ok = load_table(levels, s, smem_tab);
+    // the norm: thread t folds partials t, t + 256, ... in order, then the waves' sums in order
+    double a = 0.0;
+    uint32_t tiny = 0;
+    for (int64_t p = threadIdx.x; p < parts; p += 256) { a = ncomb<NORM>(a, partial[p]); tiny |= tinyp[p]; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a = ncomb<NORM>(a, __shfl_xor(a, o, WAVE));
+        tiny |= __shfl_xor(tiny, o, WAVE);
+    }
+    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = a; redt[threadIdx.x >> 6] = tiny; }
+    __syncthreads();
+    a = ncomb<NORM>(ncomb<NORM>(ncomb<NORM>(red[0], red[1]), red[2]), red[3]);
+    tiny = redt[0] | redt[1] | redt[2] | redt[3];
+    const float v = (NORM == FLC_NORM_L2) ? (float)sqrt(a) : (float)a;
+    const bool fast = !tiny && v >= 0x1p-40f && v <= 0x1p80f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        pn[0] = v;
+        rpn[0] = 1.0f / v;
+        rowfast[0] = fast ? 1u : 0u;
+        rk[0] = rowkey(client_key(seed, client0));
+        if (pout) pout[0] = v;
+    }
+    op.dn.b = v;
+    op.dn.rb = 1.0f / v;
+    op.dn.ok = fabsf(v) >= 0x1p-40f && fabsf(v) <= 0x1p80f;
+    op.fast = fast && tab_ok;
+    op.tab_ok = tab_ok;
+    op.urow = COMPAT ? op.us.u : nullptr;
+    op.rk = COMPAT ? 0u : rowkey(client_key(seed, client0));
+    if (op.fast) lone_dither_body<NORM, COMPAT, true>(op, x, d, smem_tab, out);
+    else lone_dither_body<NORM, COMPAT, false>(op, x, d, smem_tab, out);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -526,12 +654,15 @@ static EwWs carve_ew(void* base, int64_t n, int64_t d, size_t* bytes) {
     return w;
 }
 
+// the caller forced the sparse dithering path (flc_codec_params.flags hint)
+static bool lone_sparse(const flc_codec_params* prm) { return (prm->flags & FLC_PATH_MASK) == FLC_PATH_SPARSE; }
+
 size_t ew_workspace(const flc_codec_params* prm, int64_t n, int64_t d) {
     if (prm->codec == FLC_IDENT || prm->codec == FLC_LAZY) return 0;
     size_t b = 0;
     carve_ew(nullptr, n, d, &b);
     // fused dithering may take the sparse path (device draws; the pattern is not known here)
-    if (n > 1 && ds_eligible(prm, nullptr, n, d)) b = std::max(b, ds_workspace(prm, n, d));
+    if ((n > 1 || lone_sparse(prm)) && ds_eligible(prm, nullptr, n, d)) b = std::max(b, ds_workspace(prm, n, d));
     return b;
 }
 
@@ -543,6 +674,48 @@ static int check_dither(const flc_codec_params* prm) {
         return FLC_ERR_UNSUPPORTED;
     }
     return FLC_OK;
+}
+
+#ifndef FLC_LONE_DITHER
+#define FLC_LONE_DITHER 1
+#endif
+// compressVector of one row with standard dithering and its own norm: the partials, then
+// k_lone_dither (the norm folded in every block, the encode with its loads batched)
+static int launch_lone_dither(const flc_codec_params* prm, const UniformSrc& us, bool compat, const float* x, int64_t d,
+                              EwWs& e, float* pnorm_out, float* out, int64_t client0, hipStream_t st) {
+    const int64_t parts = (d + LONE_PLEN - 1) / LONE_PLEN;
+    const RowSrc src{x, d, nullptr};
+    const dim3 pg((unsigned)std::min<int64_t>(parts, 4096), 1);
+    const int64_t n4 = d / 4;
+    const int eg = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 256 * LONE_U - 1) / (256 * LONE_U), 2048));
+    const size_t lds = (size_t)prm->s * sizeof(float4);
+    auto go = [&](auto nk, auto cm) -> int {
+        constexpr int NK = decltype(nk)::value;
+        constexpr bool CM = decltype(cm)::value;
+        { ProfScope _ps("k_norm_partials", st);
+        hipLaunchKernelGGL((k_norm_partials<NK, true, false, (bool)FLC_LONE_KEEP>), pg, dim3(256), 0, st, src, nullptr, d, parts, LONE_PLEN,
+                           e.partial, e.tinyp); }
+        FLC_CHECK_LAUNCH("k_norm_partials");
+        DitherOp<false, CM> op;
+        op.us = us;
+        op.rt = RowTabs{e.pn, e.rpn, e.fast, e.rk};
+        op.s = prm->s;
+        op.sf = (float)prm->s;
+        op.tab_ok = false;
+        { ProfScope _ps("k_lone_dither", st);
+        hipLaunchKernelGGL((k_lone_dither<NK, CM>), dim3(eg), dim3(256), lds, st, x, d, op, prm->d_levels, prm->s, out,
+                           e.partial, e.tinyp, parts, e.pn, e.rpn, e.fast, prm->seed, client0, e.rk, pnorm_out); }
+        FLC_CHECK_LAUNCH("k_lone_dither");
+        return FLC_OK;
+    };
+    using L2 = std::integral_constant<int, FLC_NORM_L2>;
+    using L1 = std::integral_constant<int, FLC_NORM_L1>;
+    using LI = std::integral_constant<int, FLC_NORM_LINF>;
+    using T = std::true_type;
+    using Fa = std::false_type;
+    if (prm->norm == FLC_NORM_L2) return compat ? go(L2{}, T{}) : go(L2{}, Fa{});
+    if (prm->norm == FLC_NORM_L1) return compat ? go(L1{}, T{}) : go(L1{}, Fa{});
+    return compat ? go(LI{}, T{}) : go(LI{}, Fa{});
 }
 
 // One row encode (compressVector) or fused reduce over n rows (n >= 1).
@@ -562,6 +735,12 @@ int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool
     };
     if (!dense && !pnorm_in && n > 1 && ds_eligible(prm, pat, n, d))
         return ds_run(prm, pat, src, n, d, w, wt, pnorm_out, out, ws, ws_bytes, st);
+    // a lone compressVector row on the single-read sparse pass, when the caller forces it (the fold
+    // of one row with weight 1 is the row's encode, -0 included: (1 * v) / 1 == v).  Not the
+    // automatic choice: at D = 25 M the two-pass dense encode is 2.2 x faster (62 vs 218 us, device
+    // draws; the one-row fold walks every tile of the row), profiles/r04/lone_ab.txt
+    if (lone_sparse(prm) && dense && !sh && !ca && !pnorm_in && n == 1 && ds_eligible(prm, pat, 1, d))
+        return ds_run(prm, pat, src, 1, d, nullptr, 1.f, pnorm_out, out, ws, ws_bytes, st);
     if (ws_bytes < ew_workspace(prm, n, d)) { set_error("codec workspace too small"); return FLC_ERR_WORKSPACE; }
     EwWs e = carve_ew(ws, n, d, nullptr);
     switch (codec) {
@@ -589,6 +768,9 @@ int ew_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc src, bool
         case FLC_NAT_DITHERING: {
             int rc = check_dither(prm);
             if (rc) return rc;
+            if (FLC_LONE_DITHER && codec == FLC_STD_DITHERING && dense && !sh && !ca && n == 1 && !pnorm_in &&
+                ((((uintptr_t)src.base | (uintptr_t)out) & 15u) == 0) && (!compat || ((uintptr_t)us.u & 15u) == 0))
+                return launch_lone_dither(prm, us, compat, src.base, d, e, pnorm_out, out, client0, st);
             RowTabs rt{pnorm_in, nullptr, nullptr, e.rk};
             if (!pnorm_in) {
                 rc = launch_norms(src, vec, n, d, prm->norm, e.partial, e.tinyp, e.pn, e.rpn, e.fast, prm->seed,

@@ -156,6 +156,98 @@ def test_sparse_dither_row_groups(ag, monkeypatch, groups, weighted):
     assert_bitexact(got, want)
 
 
+@pytest.mark.parametrize("spec,d", [("qsgd:16", 40_003), ("qsgd:127", 300_007)])
+@pytest.mark.parametrize("entry", ["matrix", "pointers"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_sparse_dither_default_row_groups(ag, monkeypatch, spec, d, entry, weighted):
+    """Without a hint, 128 rows or more take the default two row groups (group 0's norm, resolve
+    and fold on the side stream under group 1's filter, whose blocks carry the LDS pad): same bits
+    as the oracle, through both entry points, with special rows on either side of the boundary."""
+    n, client0 = 161, 11
+    g = np.random.default_rng(161 + weighted)
+    rows = make_rows("normal", n, d, g)
+    for i, kind in ((0, "negative"), (79, "clustered"), (80, "clustered"), (81, "sparse"),
+                    (120, "heavy"), (160, "ones")):
+        rows[i] = make_rows(kind, 1, d, g)[0]
+    w = g.uniform(-1.0, 2.0, n).astype(np.float32).tolist() if weighted else None
+    want, wn = oracle_uplink(spec, rows, client0, weights=w)
+    comp = sparse(ag, spec, d)
+    assert getattr(comp, "row_groups", None) in (None, 0)
+    red = ag.UplinkReducer(comp, seed=SEED)
+    x = torch.from_numpy(rows).cuda()
+    arg = x if entry == "matrix" else [x[i] for i in range(n)]
+    pn = torch.empty(n, device="cuda")
+    got = red(arg, client0=client0, weights=w, pnorms_out=pn)
+    torch.cuda.synchronize()
+    assert_bitexact(pn, wn)
+    assert_bitexact(got, want)
+    # one filter launch per row group (a second call, so the timing events stay out of the first)
+    from flpytorch_amd import _lib
+    _lib.profile_enable(True)
+    _lib.profile_collect("k_ds_filter")
+    again = red(arg, client0=client0, weights=w)
+    torch.cuda.synchronize()
+    launches = _lib.profile_collect("k_ds_filter")[1]
+    _lib.profile_enable(False)
+    assert launches == 2
+    assert_bitexact(again, want)
+
+
+@pytest.mark.parametrize("kind", ["normal", "heavy", "sparse", "negative", "clustered", "tiny", "nan"])
+@pytest.mark.parametrize("compat", [False, True])
+@pytest.mark.parametrize("spec", ["qsgd:16", "qsgd:127"])
+def test_lone_compress_vector_sparse(ag, monkeypatch, kind, compat, spec):
+    """A lone compressVector (compressors.py:270-299) forced onto the single-read sparse pass (one
+    row folded with weight 1 is its encode, -0 included): bit-exact vs the oracle with device
+    draws and with the caller's float64 uniforms, and so is the dense two-pass encode (the
+    automatic choice for one row)."""
+    d, client = 2_000_003, 9
+    g = np.random.default_rng(zlib.crc32(f"lone{kind}{compat}{spec}".encode()))
+    x = make_rows("normal" if kind == "nan" else kind, 1, d, g)[0]
+    if kind == "nan":
+        x[1234] = np.nan
+    o = oc.OracleCompressor(spec, d)
+    c = sparse(ag, spec, d)
+    if compat:
+        u = g.random(d)
+        o.testp = u
+        c.testp = torch.from_numpy(u).cuda()
+    else:
+        o.testp = devrng.uniforms(SEED, client, d)
+        c.device_rng = (SEED, client)
+    want = o.compress(x)
+    xt = torch.from_numpy(x).cuda()
+    pn = torch.empty(1, device="cuda")
+    got = c._encode_gpu(xt, pnorm_out=pn)
+    assert_bitexact(got, want)
+    assert_bitexact(pn, np.array([o.norm(x)], dtype=np.float32))
+    assert_bitexact(c.compressVector(xt), want)
+    c.dither_path = "dense"
+    assert_bitexact(c.compressVector(xt), want)
+
+
+@pytest.mark.parametrize("compat", [False, True])
+def test_lone_compress_vector_c4_scale(ag, monkeypatch, compat):
+    """The drop-in call at C4's row length (qsgd:127, D = 25 M): the forced sparse pass and the
+    dense two-pass encode (the automatic choice) give the same bits and the same norm."""
+    d = 25_000_000
+    x = torch.empty(d, device="cuda").normal_(generator=torch.Generator("cuda").manual_seed(7))
+    c = ag.initCompressor("qsgd:127", d)
+    if compat:
+        c.testp = torch.rand(d, dtype=torch.float64, device="cuda", generator=torch.Generator("cuda").manual_seed(8))
+    else:
+        c.device_rng = (SEED, 3)
+    outs, norms = {}, {}
+    for path in ("sparse", "dense"):
+        c.dither_path = path
+        pn = torch.empty(1, device="cuda")
+        outs[path] = c._encode_gpu(x, pnorm_out=pn).cpu().numpy()
+        norms[path] = pn.cpu().numpy()
+    assert_bitexact(norms["sparse"], norms["dense"])
+    assert_bitexact(outs["sparse"], outs["dense"])
+    assert 0 < np.count_nonzero(outs["sparse"]) < d
+
+
 def test_sparse_equals_dense_c4_scale(ag, monkeypatch):
     """C4's row length (D = 25 M, qsgd:127): the sparse path and the dense two-pass path give
     the same bits, and the same norms (the oracle would take minutes at this size)."""
