@@ -222,9 +222,19 @@ __global__ __launch_bounds__(256) void k_ew_dense(const float* __restrict__ x, i
 // mode, the float64 draws' — issued before the arithmetic.  Replaces k_norm_final + k_ew_dense
 // (one launch boundary less; the grid-stride loop of k_ew_dense kept one load per thread in flight).
 // ------------------------------------------------------------------------------------------
-constexpr int64_t LONE_PLEN = 32768;          // elements per norm partial of a lone row
+// 65536-element partials (382 norm workgroups at D = 25 M), 1024 encode workgroups of 2 groups
+// per thread per trip: 88.0 -> 82.8 us per call against 32768 / 2048 / 4 (compat, D = 25 M, same
+// box; 1024 / 4 / 32768 85.2, 768 or 1536 workgroups 87.5 / 84.1, 131072-element partials 86.8),
+// profiles/r04/lone_ab.txt
+#ifndef FLC_LONE_PLEN
+#define FLC_LONE_PLEN 65536
+#endif
+#ifndef FLC_LONE_GRID
+#define FLC_LONE_GRID 1024
+#endif
+constexpr int64_t LONE_PLEN = FLC_LONE_PLEN;  // elements per norm partial of a lone row
 #ifndef FLC_LONE_U
-#define FLC_LONE_U 4
+#define FLC_LONE_U 2
 #endif
 // The norm pass reads the row with ordinary loads, so the encode's second read of it finds it in
 // the caches (the 100 MB row of C4 fits the 256 MB infinity cache), and the encode's output goes
@@ -687,7 +697,7 @@ static int launch_lone_dither(const flc_codec_params* prm, const UniformSrc& us,
     const RowSrc src{x, d, nullptr};
     const dim3 pg((unsigned)std::min<int64_t>(parts, 4096), 1);
     const int64_t n4 = d / 4;
-    const int eg = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 256 * LONE_U - 1) / (256 * LONE_U), 2048));
+    const int eg = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 256 * LONE_U - 1) / (256 * LONE_U), FLC_LONE_GRID));
     const size_t lds = (size_t)prm->s * sizeof(float4);
     auto go = [&](auto nk, auto cm) -> int {
         constexpr int NK = decltype(nk)::value;

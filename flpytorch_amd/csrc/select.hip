@@ -84,16 +84,21 @@ __device__ inline void hist_find_at(const uint32_t* h, uint32_t k, uint32_t& bin
 #pragma unroll
     for (int q = 0; q < 8; ++q) { local[q] = own ? h[HBINS - 1 - (t * 8 + q)] : 0u; s += local[q]; }
     if (t == 0) { scratch[256] = 0; scratch[257] = 0; }   // defined result even if k > total
-    if (own) scratch[t] = s;
-    __syncthreads();
-    // inclusive scan (Hillis-Steele) over 256 thread sums
-    for (int off = 1; off < 256; off <<= 1) {
-        uint32_t v = (own && t >= off) ? scratch[t - off] : 0u;
-        __syncthreads();
-        if (own) scratch[t] += v;
-        __syncthreads();
+    // inclusive scan over the 256 thread sums: inside each wave by shuffles, then the totals of the
+    // waves before (one barrier instead of the 16 of a Hillis-Steele scan through LDS)
+    const int lane = t & 63, w = t >> 6;
+    uint32_t inc = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off, 64);
+        inc += lane >= off ? v : 0u;
     }
-    uint32_t incl = own ? scratch[t] : 0u, excl = incl - s;
+    if (own && lane == 63) scratch[w] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    if (own)
+        for (int q = 0; q < w; ++q) before += scratch[q];
+    uint32_t incl = own ? before + inc : 0u, excl = incl - s;
     if (own && excl < k && incl >= k) {
         uint32_t run = excl;
 #pragma unroll
