@@ -45,6 +45,14 @@ constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
 constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
 constexpr int CS_SH = 64;            // few rows: shards of a row's candidate list (k_cs_pass workgroups)
 constexpr int64_t CS_FEW = 16;       // rows: sharded lists + k_cs_pass up to here, else k_cand_select
+constexpr int CS_ST = 8;             // words of a row's k_cs_pass state
+constexpr int CS_LCAP = 2048;        // entries of the first digit's bin ranked directly (list mode)
+#ifndef FLC_CS_LIST
+#define FLC_CS_LIST 1
+#endif
+#ifndef FLC_CS_TWO_MAXD
+#define FLC_CS_TWO_MAXD (int64_t(64) << 20)   // rows up to this long: two k_cs_pass launches
+#endif
 
 struct SelWs {            // carved from the caller workspace
     uint2* tab;           // [C][N] (offset, count) of each row's entries in chunk c
@@ -61,7 +69,8 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* worklist;   // [N] rows on the exact path
     uint32_t* nwork;      // [1]
     uint32_t* cursor;     // [C][N] RandK scatter cursors
-    uint32_t* cstate;     // [N][4] few-row candidate select: shift, prefix, krem, stage (k_cs_pass)
+    uint32_t* cstate;     // [N][CS_ST] few-row candidate select: shift, prefix, krem, stage, bin count, list fill (k_cs_pass)
+    uint64_t* clist;      // [min(N, CS_FEW)][CS_LCAP] few rows: the first digit bin's entries (k_cs_pass list mode)
     uint32_t* carrive;    // [N * RCS] its per-row arrival counters
     uint32_t* shcnt;      // [N][CS_SH * RCS] few rows: the filter's reservation counters, one per shard
     uint32_t* zm;         // [C][CHUNK / 32] k_chunk_accum (one-wave blocks): a fold job's kept-column mask
@@ -249,7 +258,7 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
         ws.prefix[row] = kest;
         ws.flags[row] = 0;
         ws.rowcnt[(row) * RCS] = 0;
-        if (few) { ws.cstate[row * 4 + 3] = 0; ws.carrive[row * RCS] = 0; }
+        if (few) { ws.cstate[row * CS_ST + 3] = 0; ws.cstate[row * CS_ST + 5] = 0; ws.carrive[row * RCS] = 0; }
     }
     if (few && threadIdx.x < CS_SH) ws.shcnt[(row * CS_SH + threadIdx.x) * RCS] = 0;
     if (few)                                              // the row's global histogram of k_cs_pass
@@ -402,13 +411,19 @@ __global__ __launch_bounds__(NT) void k_cand_select(int64_t r0, int64_t rn, int6
 // the exact path.
 // ------------------------------------------------------------------------------------------
 constexpr int CS_NT = 256;
-__global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
+// final_pass: no launch follows this one (a row the digits have not settled by then takes the exact
+// path); list mode (second pass, the first digit's bin holding at most CS_LCAP entries): every
+// workgroup copies its shard's entries of that bin to the row's list and the last arriver ranks them
+// by (key desc, index asc) — the K-th key and the tie cut at once, whatever bits are left below the
+// first digit, so two launches settle the row.
+__global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws, int final_pass) {
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
     __shared__ uint32_t last_wg;
+    __shared__ uint64_t lst[FLC_CS_LIST ? CS_LCAP : 1];
     const int64_t row = blockIdx.y;
     const uint32_t B = gridDim.x, b = blockIdx.x;
-    uint32_t* cs = ws.cstate + row * 4;                                 // shift, prefix, krem, stage
+    uint32_t* cs = ws.cstate + row * CS_ST;                              // shift, prefix, krem, stage, bin count, list fill
     const uint32_t stage = cs[3];
     if (stage >= 2u) return;                                             // done: the whole grid row
     // the row's list is CS_SH shards (the filter's reservations): workgroup b walks shard b
@@ -436,6 +451,75 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
     }
     const uint32_t s1 = first ? sh : (sh > 11u ? sh - 11u : 0u);
     const uint32_t mask = first ? 0xFFFFFFFFu : ((1u << (sh - s1)) - 1u);
+    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
+    if (FLC_CS_LIST && !first && cs[4] <= (uint32_t)CS_LCAP) {
+        // list mode: this shard's entries of the first digit's bin, as (key << 32 | ~index)
+        if (threadIdx.x == 0) scratch[0] = 0;
+        __syncthreads();
+        const float* sv = ws.ent_val + row * ws.cap + b * segcap;
+        const uint32_t* si = ws.ent_idx + row * ws.cap + b * segcap;
+        for (uint32_t e = threadIdx.x; e < mycnt; e += CS_NT) {
+            const uint32_t key = mag_key(sv[e]);
+            if (((key - T) >> sh) == prefix) {
+                const uint32_t slot = atomicAdd(&scratch[0], 1u);
+                if (slot < (uint32_t)CS_LCAP) lst[slot] = ((uint64_t)key << 32) | (uint64_t)(~si[e]);
+            }
+        }
+        __syncthreads();
+        const uint32_t nl = min(scratch[0], (uint32_t)CS_LCAP);
+        if (threadIdx.x == 0) scratch[1] = nl ? atomicAdd(&cs[5], nl) : 0u;
+        __syncthreads();
+        uint64_t* gl = ws.clist + row * CS_LCAP;
+        const uint32_t gb = scratch[1];
+        for (uint32_t i = threadIdx.x; i < nl; i += CS_NT)
+            if (gb + i < (uint32_t)CS_LCAP) gl[gb + i] = lst[i];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            last_wg = atomicAdd(&ws.carrive[row * RCS], 1u) == B - 1u ? 1u : 0u;
+        }
+        __syncthreads();
+        if (!last_wg) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t m = __hip_atomic_load(&cs[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool ok = m == cs[4] && m >= krem && krem >= 1u;          // every entry of the bin arrived
+        const uint32_t mm = min(m, (uint32_t)CS_LCAP);
+        for (uint32_t i = threadIdx.x; i < mm; i += CS_NT)
+            lst[i] = __hip_atomic_load(&gl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) { scratch[0] = 0; scratch[1] = 0; scratch[2] = 0; scratch[3] = 0; }
+        __syncthreads();
+        // the entry of rank krem - 1 is the K-th: its key the threshold, its index the tie cut
+        if (ok)
+            for (uint32_t i = threadIdx.x; i < mm; i += CS_NT) {
+                const uint64_t me = lst[i];
+                uint32_t rank = 0;
+                for (uint32_t j = 0; j < mm; ++j) rank += lst[j] > me ? 1u : 0u;
+                if (rank == krem - 1u) { scratch[0] = (uint32_t)(me >> 32); scratch[1] = ~(uint32_t)me; }
+            }
+        __syncthreads();
+        const uint32_t kth = scratch[0];
+        if (ok)
+            for (uint32_t i = threadIdx.x; i < mm; i += CS_NT) {
+                const uint32_t key = (uint32_t)(lst[i] >> 32);
+                if (key > kth) atomicAdd(&scratch[2], 1u);
+                else if (key == kth) atomicAdd(&scratch[3], 1u);
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            atomicExch(&ws.carrive[row * RCS], 0u);
+            if (!ok) {
+                ws.flags[row] |= F_SHORT;                                // exact path
+            } else {
+                const uint32_t gt = scratch[2], eq = scratch[3];
+                ws.thr[row] = kth;
+                ws.krem[row] = krem - gt;                                // ties admitted
+                if (gt + eq > krem) { ws.tiecut[row] = scratch[1]; ws.flags[row] |= F_TIES; }
+            }
+            cs[3] = 2u;
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < HBINS; i += CS_NT) h[i] = 0;
     __syncthreads();
     auto add = [&](float x) {
@@ -443,7 +527,6 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
         if (first) atomicAdd(&h[min(dk >> s1, (uint32_t)(HBINS - 1))], 1u);
         else if ((dk >> sh) == prefix) atomicAdd(&h[(dk >> s1) & mask], 1u);
     };
-    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
     const float* vals = ws.ent_val + row * ws.cap + b * segcap;          // 16 B aligned shards
     const float4* v4 = reinterpret_cast<const float4*>(vals);
     const uint32_t n4 = mycnt >> 2, q1 = n4;
@@ -544,8 +627,11 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws) {
                 if (ties) ws.flags[row] |= F_TIES;
             }
             cs[3] = 2u;
+        } else if (final_pass) {
+            ws.flags[row] |= F_SHORT;                                    // digits left, no launch: exact path
+            cs[3] = 2u;
         } else {
-            cs[0] = s1; cs[1] = np; cs[2] = nk; cs[3] = 1u;
+            cs[0] = s1; cs[1] = np; cs[2] = nk; cs[3] = 1u; cs[4] = last;
         }
     }
 }
@@ -2200,7 +2286,8 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tiecut = cv.take<uint32_t>(nn);
         s.hist = cv.take<uint32_t>((size_t)nn * HBINS);
         s.cursor = nullptr;
-        s.cstate = cv.take<uint32_t>((size_t)nn * 4);
+        s.cstate = cv.take<uint32_t>((size_t)nn * CS_ST);
+        s.clist = cv.take<uint64_t>((size_t)std::min<int64_t>(nn, CS_FEW) * CS_LCAP);
         s.carrive = cv.take<uint32_t>((size_t)nn * RCS);
         s.shcnt = cv.take<uint32_t>((size_t)std::min<int64_t>(nn, CS_FEW) * CS_SH * RCS);
     } else {
@@ -2209,6 +2296,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.hist = nullptr;
         s.cursor = cv.take<uint32_t>((size_t)std::max<int64_t>(C, RK_SB) * nn);   // RandK: [N][RK_SB] segment offsets
         s.cstate = nullptr;
+        s.clist = nullptr;
         s.carrive = nullptr;
         s.shcnt = nullptr;
     }
@@ -2545,11 +2633,15 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 }
                 { ProfScope _ps("k_cand_select", sside);
                 // few rows (a lone compressVector): each list over 64 workgroups, one launch per
-                // digit (3 cover every shift; a finished row's workgroups exit at once); many rows:
-                // 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
+                // digit (a finished row's workgroups exit at once); with list mode two launches
+                // settle a row whose first digit's bin holds <= CS_LCAP entries (~(4 sqrt(ks) + 8)
+                // D / 16 K spread over 256-512 bins: up to ~900 at D = 64 M), else 3 cover every
+                // shift; many rows: 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
                 if (few) {
-                    for (int p = 0; p < 3; ++p)
-                        hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws);
+                    const int np = (FLC_CS_LIST && d <= FLC_CS_TWO_MAXD) ? 2 : 3;
+                    for (int p = 0; p < np; ++p)
+                        hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws,
+                                           p == np - 1 ? 1 : 0);
                 } else if (gfold) {
                     // the select with the exact fallback in the same workgroup (every row final after
                     // it), then the group's rows folded into the running tiles, both on the side stream

@@ -402,6 +402,21 @@ def test_topk_lone_row_vs_oracle(ag, kind, d, k):
     assert_bitexact(c.compressVector(buf[1:]), want)
 
 
+@pytest.mark.parametrize("kind", ["normal", "heavy"])
+def test_topk_lone_row_three_passes(ag, kind):
+    """A lone row longer than FLC_CS_TWO_MAXD (64 Mi): the candidate select keeps its third
+    k_cs_pass launch (the first digit's bin may hold more entries than list mode ranks).
+    Bit-exact vs the oracle, off the exact path."""
+    d, k = (64 << 20) + 4099, 700_001
+    g = np.random.default_rng([d, len(kind)])
+    x = _topk_rows(kind, 1, d, g)[0]
+    want = _topk_enc([x], k)[0]
+    c = ag.initCompressor(f"topk:{k}", d)
+    assert_bitexact(c.compressVector(torch.from_numpy(x).cuda()), want)
+    f = int(ag.select_row_flags(c, 1, d)[0])
+    assert f & 8 == 0, f"flags {f}: the row took the exact path"
+
+
 @pytest.mark.parametrize("ties", [20, 600, 1500, 3000])
 def test_topk_lone_row_tie_capacity(ag, ties):
     """The lone row's tie cut (k_cs_pass's last arriver gathers the indices of the entries equal to
