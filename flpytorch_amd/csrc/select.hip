@@ -2371,6 +2371,9 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
 #ifndef FLC_TK_LASTPCT
 #define FLC_TK_LASTPCT 100            // size of the last TopK row group in % of the others (its tail is exposed)
 #endif
+#ifndef FLC_TK_LAST_TS
+#define FLC_TK_LAST_TS 4096           // the exposed last group fold's tile (columns per wave)
+#endif
 #ifndef FLC_TK_GFOLD
 #define FLC_TK_GFOLD 1                // many-row TopK: fold each row group under the next group's filter
 #endif
@@ -2386,8 +2389,10 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
 // with 4, 8.04 with 8; profiles/r03/ab_tailov.txt); tuning builds FLC_TK_TAILOV=g.  (The same
 // overlap of the sparse QSGD norm + resolve lost at C4, 10.20 -> 10.27-10.44 ms: its filter split
 // in groups runs slower; it stays a tuning knob there, FLC_DS_TAILOV.)
-static int tk_tail_groups(int64_t n) {
+static int tk_tail_groups(const flc_codec_params* prm, int64_t n) {
     static const int g = [] { const char* e = tuning_env("FLC_TK_TAILOV"); return e ? std::max(1, atoi(e)) : 4; }();
+    const int hint = (prm->flags >> 8) & 0xFF;                       // FLC_ROW_GROUPS(g): the caller's
+    if (hint) return (int)std::max<int64_t>(1, std::min<int64_t>(hint, n));
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, n / 64));
 }
 namespace {
@@ -2504,10 +2509,11 @@ static int launch_group_fold(int64_t n, int64_t d, SelWs ws, const float* w, flo
         else hipLaunchKernelGGL((k_chunk_accum1<false>), dim3(ab), dim3(64), CHUNK * sizeof(float), st, n, d, ws, w, wt, out, r0, r1,
                                 first ? 1 : 0, last ? 1 : 0);
     } else {
-        const int ab = grid_stride_blocks((C + 3) / 4, 4096);
-        if (w) hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out, r0, r1,
+        constexpr int LTS = FLC_TK_LAST_TS;
+        const int ab = grid_stride_blocks((C * (CHUNK / LTS) + 3) / 4, 4096);
+        if (w) hipLaunchKernelGGL((k_chunk_accum<false, LTS, true>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out, r0, r1,
                                   first ? 1 : 0, last ? 1 : 0);
-        else hipLaunchKernelGGL((k_chunk_accum<false, CHUNK, false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out, r0, r1,
+        else hipLaunchKernelGGL((k_chunk_accum<false, LTS, false>), dim3(ab), dim3(256), 0, st, n, d, ws, w, wt, out, r0, r1,
                                 first ? 1 : 0, last ? 1 : 0);
     }
     FLC_CHECK_LAUNCH("k_chunk_accum(group)");
@@ -2593,7 +2599,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             // per row group: filter (the full read), then the candidate select and the exact
             // fallback of the group's rows; with TG > 1 groups the select + fallback of group g run
             // on a side stream under the filter of group g + 1 (both per-row, other rows' lists)
-            const int TG = few ? 1 : tk_tail_groups(n);
+            const int TG = few ? 1 : tk_tail_groups(prm, n);
             // many rows: each group's select does its own exact fallback and its rows are folded
             // right after it (tiles carried in ws.part), under the next group's filter
             gfold = FLC_TK_GFOLD && !few && !assign && !dense_k;

@@ -58,10 +58,11 @@ typedef enum {
 
 /* Execution hints (flc_codec_params.flags).  They choose HOW a result is computed, never WHAT:
  * every combination gives the same bits.  0 = the library's choice.
- *   bits 0-1  dithering p = 2 in device-RNG mode: FLC_PATH_SPARSE (one-read candidate filter +
- *             exact fold) or FLC_PATH_DENSE (norm pass, then encode pass)
- *   bits 8-15 fused encode+reduce: number of row groups whose folds are pipelined under the
- *             next group's streaming pass (FLC_ROW_GROUPS(g), g in 1..255) */
+ *   bits 0-1  standard dithering with p = 2: FLC_PATH_SPARSE (one-read candidate filter + exact
+ *             fold) or FLC_PATH_DENSE (norm pass, then encode pass); flc_encode of one row takes
+ *             the sparse pass only when FLC_PATH_SPARSE is set
+ *   bits 8-15 fused encode+reduce (QSGD sparse path, TopK): number of row groups whose tails are
+ *             pipelined under the next group's streaming pass (FLC_ROW_GROUPS(g), g in 1..255) */
 #define FLC_PATH_AUTO 0
 #define FLC_PATH_SPARSE 1
 #define FLC_PATH_DENSE 2
