@@ -10,6 +10,12 @@ namespace flc {
 // tools/probe_filter.hip), so each row's counter has a 128 B line of its own.
 constexpr int RCS = 32;
 
+// The folds' carried tiles (row groups after the first) loaded with all their loads in flight
+// (k_chunk_accum, k_ds_accum); 0: the per-64-column load -> LDS write loop
+#ifndef FLC_TILE_V4
+#define FLC_TILE_V4 1
+#endif
+
 __host__ __device__ inline int64_t nchunks(int64_t d) { return (d + CHUNK - 1) >> CHUNK_SHIFT; }
 
 // Buffer descriptor of one chunk built from the wave-uniform chunk base (SGPRs): 32-bit lane

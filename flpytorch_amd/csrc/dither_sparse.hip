@@ -1214,7 +1214,18 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
         // each column sees its rows' terms in row order.
         const uint32_t hbase = (uint32_t)(h * HCHUNK);
         const int64_t len = min((int64_t)HCHUNK, d - (int64_t)hbase);
-        for (int i = lane; i < HCHUNK; i += 64) tl[i] = (first || i >= len) ? -0.f : part[hbase + i];
+        if (FLC_TILE_V4 && !first && len == HCHUNK) {
+            // the carried tile with every load in flight at once (the loop of load -> LDS write
+            // pairs below waits one memory latency per 64 columns: 32 per tile)
+            const float4* p4 = reinterpret_cast<const float4*>(part + hbase);
+            float4 v[HCHUNK / 256];
+#pragma unroll
+            for (int k = 0; k < HCHUNK / 256; ++k) v[k] = p4[k * 64 + lane];
+#pragma unroll
+            for (int k = 0; k < HCHUNK / 256; ++k) reinterpret_cast<float4*>(tl)[k * 64 + lane] = v[k];
+        } else {
+            for (int i = lane; i < HCHUNK; i += 64) tl[i] = (first || i >= len) ? -0.f : part[hbase + i];
+        }
         DsMeta cur = ds_meta(ws, h, n, rend, r0 + lane, w), nxt;
         uint32_t ra[AP];                        // ring: first 64 entries of rows q .. q + AP - 1
         // a list's 64-entry window never leaves its item's half region (DS_HCAP >= 64): loaded

@@ -1725,8 +1725,23 @@ __device__ __forceinline__ void chunk_accum_body(int64_t n, int64_t d, SelWs ws,
         const int64_t c = t / PARTS;
         const uint32_t cbase = (uint32_t)(c * CHUNK + (t % PARTS) * TS);
         // ASSIGN (compressVector: out = zeros, out[kept] = x) stores into +0; the fold adds into -0
-        for (int i = lane; i < TS; i += 64)
-            tl[i] = ASSIGN ? 0.f : (first || (int64_t)cbase + i >= d ? -0.f : ws.part[cbase + i]);
+        if (FLC_TILE_V4 && !ASSIGN && !first && (int64_t)cbase + TS <= d) {
+            // the carried tile with its loads in flight 8 float4 at a time (the loop of load -> LDS
+            // write pairs below waits one memory latency per 64 columns: 64 per 4096-column tile)
+            const float4* p4 = reinterpret_cast<const float4*>(ws.part + cbase);
+#pragma unroll
+            for (int k0 = 0; k0 < TS / 256; k0 += 8) {
+                float4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = k0 + k < TS / 256 ? p4[(k0 + k) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k0 + k < TS / 256) reinterpret_cast<float4*>(tl)[(k0 + k) * 64 + lane] = v[k];
+            }
+        } else {
+            for (int i = lane; i < TS; i += 64)
+                tl[i] = ASSIGN ? 0.f : (first || (int64_t)cbase + i >= d ? -0.f : ws.part[cbase + i]);
+        }
         RowMeta cur = load_meta(ws, c, n, r0 + lane, w, rend), nxt;
         // ring of AP rows' entries (the first 128 of each list; range-checked buffer loads, lanes
         // past the list end get index ~0 = no column)

@@ -1,0 +1,105 @@
+// Stand-alone probe (not part of libflcodec): the C4 fold's list walk (k_ds_accum) without its
+// arithmetic, to tell the access pattern's own cost from the kernel's.  One 64-lane workgroup per
+// half-chunk tile (H = 12207 at D = 25 M) with an 8 KB LDS tile (the fold's occupancy), walking
+// n = 256 rows with a 16-row register ring; loads are summed, nothing else.
+//
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/probe_walk.hip -o tools/probe_walk
+//   tools/probe_walk [H=12207] [n=256] [reps=5]
+//
+// modes:  fixed   the product layout: row r of tile h at (h n + r) 256 B, the first 128 B read
+//                 (64 u16 entries, one per lane)
+//         packed  the same entries with the rows of a tile contiguous at 96 B each (48 entries:
+//                 the C4 lists hold ~41), lanes >= 48 idle
+//         lds     fixed, plus the fold's per-row LDS read-modify-write of the tile (64 distinct
+//                 columns per row, rows in order)
+//         dense   each wave streams its tile's whole 64 KB region with 16-B-per-lane loads
+//                 (1 KB per load, 16 in flight): the bytes-in-flight bound of the same footprint
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+constexpr int AP = 16;
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_walk(const uint8_t* __restrict__ base, int64_t H, int64_t n, uint32_t* out) {
+    extern __shared__ float tile[];
+    const int lane = threadIdx.x;
+    const int64_t h = blockIdx.x;
+    if (h >= H) return;
+    for (int i = lane; i < 2048; i += 64) tile[i] = 0.f;
+    uint32_t acc = 0;
+    if (MODE == 2) {
+        const uint4* p = reinterpret_cast<const uint4*>(base + h * n * 256);
+        const int64_t nl = n * 256 / 1024;             // 1 KB per wave load
+        uint4 r[AP];
+#pragma unroll
+        for (int u = 0; u < AP; ++u) r[u] = u < nl ? p[u * 64 + lane] : make_uint4(0, 0, 0, 0);
+        for (int64_t q = 0; q < nl; q += AP) {
+#pragma unroll
+            for (int u = 0; u < AP; ++u) {
+                acc += r[u].x ^ r[u].y ^ r[u].z ^ r[u].w;
+                const int64_t nq = q + AP + u;
+                r[u] = nq < nl ? p[nq * 64 + lane] : make_uint4(0, 0, 0, 0);
+            }
+        }
+    } else {
+        const int64_t rs = MODE != 1 ? 256 : 96;       // bytes per row region
+        const int ne = MODE != 1 ? 64 : 48;
+        const uint16_t* p = reinterpret_cast<const uint16_t*>(base + (MODE != 1 ? h * n * 256 : h * n * 96));
+        uint32_t r[AP];
+#pragma unroll
+        for (int u = 0; u < AP; ++u) r[u] = lane < ne ? p[u * (rs / 2) + lane] : 0u;
+        for (int64_t q = 0; q < n; q += AP) {
+#pragma unroll
+            for (int u = 0; u < AP; ++u) {
+                acc += r[u];
+                if (MODE == 3) {
+                    const uint32_t loc = ((uint32_t)lane * 37u + (uint32_t)(q + u) * 11u + r[u]) & 2047u;
+                    tile[loc] = tile[loc] + 1.0f;
+                }
+                const int64_t nq = q + AP + u;
+                r[u] = (nq < n && lane < ne) ? p[nq * (rs / 2) + lane] : 0u;
+            }
+        }
+    }
+    tile[lane] += (float)acc;
+    if (tile[lane] == 1234.5f) out[h] = acc;
+}
+
+int main(int argc, char** argv) {
+    const int64_t H = argc > 1 ? atoll(argv[1]) : 12207, n = argc > 2 ? atoll(argv[2]) : 256;
+    const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const size_t bytes = (size_t)H * n * 256;
+    uint8_t* base;
+    uint32_t* out;
+    CK(hipMalloc(&base, bytes));
+    CK(hipMalloc(&out, H * 4));
+    CK(hipMemset(base, 1, bytes));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const char* names[4] = {"fixed", "packed", "dense", "lds"};
+    const double moved[4] = {(double)H * n * 128, (double)H * n * 96, (double)H * n * 256, (double)H * n * 128};
+    for (int rep = 0; rep < reps; ++rep) {
+        for (int m = 0; m < 4; ++m) {
+            CK(hipEventRecord(e0, 0));
+            if (m == 0) hipLaunchKernelGGL(k_walk<0>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
+            if (m == 1) hipLaunchKernelGGL(k_walk<1>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
+            if (m == 2) hipLaunchKernelGGL(k_walk<2>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
+            if (m == 3) hipLaunchKernelGGL(k_walk<3>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
+            CK(hipGetLastError());
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("{\"rep\": %d, \"mode\": \"%s\", \"us\": %.1f, \"GBps_read\": %.0f}\n", rep, names[m], ms * 1e3,
+                   moved[m] / (ms * 1e-3) / 1e9);
+        }
+    }
+    CK(hipFree(base));
+    CK(hipFree(out));
+    return 0;
+}
