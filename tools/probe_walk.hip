@@ -12,6 +12,8 @@
 //                 the C4 lists hold ~41), lanes >= 48 idle
 //         lds     fixed, plus the fold's per-row LDS read-modify-write of the tile (64 distinct
 //                 columns per row, rows in order)
+//         meta    lds, plus the fold's per-batch row state: a u32 per row loaded one 64-row batch
+//                 ahead, whose value (readlane) picks each refill's address (k_ds_accum's cnt)
 //         dense   each wave streams its tile's whole 64 KB region with 16-B-per-lane loads
 //                 (1 KB per load, 16 in flight): the bytes-in-flight bound of the same footprint
 #include <hip/hip_runtime.h>
@@ -24,14 +26,40 @@
 constexpr int AP = 16;
 
 template <int MODE>
-__global__ __launch_bounds__(64) void k_walk(const uint8_t* __restrict__ base, int64_t H, int64_t n, uint32_t* out) {
+__global__ __launch_bounds__(64) void k_walk(const uint8_t* __restrict__ base, int64_t H, int64_t n, uint32_t* out,
+                                             const uint32_t* __restrict__ mbase) {
     extern __shared__ float tile[];
     const int lane = threadIdx.x;
     const int64_t h = blockIdx.x;
     if (h >= H) return;
     for (int i = lane; i < 2048; i += 64) tile[i] = 0.f;
     uint32_t acc = 0;
-    if (MODE == 2) {
+    if (MODE == 4) {
+        const uint32_t* meta = mbase + h * n;
+        const uint16_t* p = reinterpret_cast<const uint16_t*>(base + h * n * 256);
+        uint32_t cur = meta[lane], nxt = 0;
+        uint32_t r[AP];
+#pragma unroll
+        for (int u = 0; u < AP; ++u) {
+            const uint32_t c = __builtin_amdgcn_readlane(cur, u);
+            r[u] = p[(c ? u : 0) * 128 + lane];
+        }
+        for (int64_t b = 0; b < n / 64; ++b) {
+            nxt = (b + 1) * 64 + lane < n ? meta[(b + 1) * 64 + lane] : 0u;
+#pragma unroll
+            for (int q = 0; q < 64; ++q) {
+                const int u = q % AP;
+                acc += r[u];
+                const uint32_t loc = ((uint32_t)lane * 37u + (uint32_t)q * 11u + r[u]) & 2047u;
+                tile[loc] = tile[loc] + 1.0f;
+                const int nq = q + AP;
+                const uint32_t c = nq < 64 ? __builtin_amdgcn_readlane(cur, nq) : __builtin_amdgcn_readlane(nxt, nq - 64);
+                const int64_t row = b * 64 + nq;
+                r[u] = (row < n && c) ? (uint32_t)p[row * 128 + lane] : 0u;
+            }
+            cur = nxt;
+        }
+    } else if (MODE == 2) {
         const uint4* p = reinterpret_cast<const uint4*>(base + h * n * 256);
         const int64_t nl = n * 256 / 1024;             // 1 KB per wave load
         uint4 r[AP];
@@ -81,15 +109,19 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[4] = {"fixed", "packed", "dense", "lds"};
-    const double moved[4] = {(double)H * n * 128, (double)H * n * 96, (double)H * n * 256, (double)H * n * 128};
+    uint32_t* meta;
+    CK(hipMalloc(&meta, (size_t)H * n * 4));
+    CK(hipMemset(meta, 1, (size_t)H * n * 4));
+    const char* names[5] = {"fixed", "packed", "dense", "lds", "meta"};
+    const double moved[5] = {(double)H * n * 128, (double)H * n * 96, (double)H * n * 256, (double)H * n * 128, (double)H * n * 128};
     for (int rep = 0; rep < reps; ++rep) {
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < 5; ++m) {
             CK(hipEventRecord(e0, 0));
-            if (m == 0) hipLaunchKernelGGL(k_walk<0>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
-            if (m == 1) hipLaunchKernelGGL(k_walk<1>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
-            if (m == 2) hipLaunchKernelGGL(k_walk<2>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
-            if (m == 3) hipLaunchKernelGGL(k_walk<3>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out);
+            if (m == 0) hipLaunchKernelGGL(k_walk<0>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
+            if (m == 1) hipLaunchKernelGGL(k_walk<1>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
+            if (m == 2) hipLaunchKernelGGL(k_walk<2>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
+            if (m == 3) hipLaunchKernelGGL(k_walk<3>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
+            if (m == 4) hipLaunchKernelGGL(k_walk<4>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
             CK(hipGetLastError());
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
@@ -101,5 +133,6 @@ int main(int argc, char** argv) {
     }
     CK(hipFree(base));
     CK(hipFree(out));
+    CK(hipFree(meta));
     return 0;
 }
