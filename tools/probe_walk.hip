@@ -14,6 +14,7 @@
 //                 columns per row, rows in order)
 //         meta    lds, plus the fold's per-batch row state: a u32 per row loaded one 64-row batch
 //                 ahead, whose value (readlane) picks each refill's address (k_ds_accum's cnt)
+//         ldsrand lds with each row's 64 distinct columns at random banks (lane * 32 + a hash < 32)
 //         dense   each wave streams its tile's whole 64 KB region with 16-B-per-lane loads
 //                 (1 KB per load, 16 in flight): the bytes-in-flight bound of the same footprint
 #include <hip/hip_runtime.h>
@@ -24,6 +25,10 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 constexpr int AP = 16;
+__device__ inline uint32_t hmix(uint32_t v) {
+    v *= 2654435761u; v ^= v >> 16; v *= 0x85EBCA6Bu; v ^= v >> 13; v *= 0xC2B2AE35u; v ^= v >> 16;
+    return v;
+}
 
 template <int MODE>
 __global__ __launch_bounds__(64) void k_walk(const uint8_t* __restrict__ base, int64_t H, int64_t n, uint32_t* out,
@@ -74,7 +79,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t* __restrict__ base, i
             }
         }
     } else {
-        const int64_t rs = MODE != 1 ? 256 : 96;       // bytes per row region
+        const int64_t rs = MODE != 1 ? 256 : 96;   // (modes 0, 3, 5: the product layout)       // bytes per row region
         const int ne = MODE != 1 ? 64 : 48;
         const uint16_t* p = reinterpret_cast<const uint16_t*>(base + (MODE != 1 ? h * n * 256 : h * n * 96));
         uint32_t r[AP];
@@ -84,8 +89,10 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t* __restrict__ base, i
 #pragma unroll
             for (int u = 0; u < AP; ++u) {
                 acc += r[u];
-                if (MODE == 3) {
-                    const uint32_t loc = ((uint32_t)lane * 37u + (uint32_t)(q + u) * 11u + r[u]) & 2047u;
+                if (MODE == 3 || MODE == 5) {
+                    // 3: 64 distinct banks per row; 5: hashed columns (distinct, random banks, as real lists)
+                    const uint32_t loc = MODE == 3 ? (((uint32_t)lane * 37u + (uint32_t)(q + u) * 11u + r[u]) & 2047u)
+                                                   : (((uint32_t)lane * 32u + (hmix((uint32_t)(q + u) * 64u + (uint32_t)lane) >> 27)) & 2047u);
                     tile[loc] = tile[loc] + 1.0f;
                 }
                 const int64_t nq = q + AP + u;
@@ -112,16 +119,17 @@ int main(int argc, char** argv) {
     uint32_t* meta;
     CK(hipMalloc(&meta, (size_t)H * n * 4));
     CK(hipMemset(meta, 1, (size_t)H * n * 4));
-    const char* names[5] = {"fixed", "packed", "dense", "lds", "meta"};
-    const double moved[5] = {(double)H * n * 128, (double)H * n * 96, (double)H * n * 256, (double)H * n * 128, (double)H * n * 128};
+    const char* names[6] = {"fixed", "packed", "dense", "lds", "meta", "ldsrand"};
+    const double moved[6] = {(double)H * n * 128, (double)H * n * 96, (double)H * n * 256, (double)H * n * 128, (double)H * n * 128, (double)H * n * 128};
     for (int rep = 0; rep < reps; ++rep) {
-        for (int m = 0; m < 5; ++m) {
+        for (int m = 0; m < 6; ++m) {
             CK(hipEventRecord(e0, 0));
             if (m == 0) hipLaunchKernelGGL(k_walk<0>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
             if (m == 1) hipLaunchKernelGGL(k_walk<1>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
             if (m == 2) hipLaunchKernelGGL(k_walk<2>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
             if (m == 3) hipLaunchKernelGGL(k_walk<3>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
             if (m == 4) hipLaunchKernelGGL(k_walk<4>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
+            if (m == 5) hipLaunchKernelGGL(k_walk<5>, dim3((unsigned)H), dim3(64), 8192, 0, base, H, n, out, meta);
             CK(hipGetLastError());
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
