@@ -1,5 +1,7 @@
 #!/bin/bash
 # k_ds_accum end-of-fold cost probes (outputs not valid): e1 without the -0 pass, e2 also without the division
+# (the FLC_DS_PROBE_END switch of these probe builds was a temporary patch of k_ds_accum, not kept in the tree:
+#  1 = the untouched-column pass skipped, 2 = also out = tile without the division by w_total)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 o=gpurun_out/endp; mkdir -p $o
