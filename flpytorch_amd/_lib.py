@@ -41,7 +41,7 @@ EXPORTS = [
     "flc_device_uniform", "flc_device_randk_indices",
     "flc_device_randk_counts_workspace_size", "flc_device_randk_counts",
     "flc_profile_enable", "flc_profile_collect", "flc_select_row_flags",
-    "flc_selftest_division",
+    "flc_selftest_division", "flc_norm2_torch_cpu",
 ]
 
 
@@ -173,6 +173,8 @@ def _bind(lib):
     lib.flc_profile_enable.argtypes = [i32]
     lib.flc_profile_collect.argtypes = [ctypes.c_char_p, vp, vp]
     lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
+    if hasattr(lib, "flc_norm2_torch_cpu"):         # (absent from A/B builds of older revisions)
+        lib.flc_norm2_torch_cpu.argtypes = [vp, i64, i64, i64, vp, vp]
     if hasattr(lib, "flc_select_row_flags"):        # (absent from A/B builds of older revisions)
         lib.flc_select_row_flags.argtypes = [P(FlcCodecParams), i64, i64, vp, sz, vp, vp]
     for name in EXPORTS:
@@ -260,7 +262,14 @@ def stream_ptr(device=None):
 
 
 class Workspace:
-    """Per-device scratch for the library (grown on demand, reused across calls)."""
+    """Per-(device, stream) scratch for the library (grown on demand, reused across calls).
+
+    Keyed by the CURRENT stream, not the thread: calls queued on one stream run in
+    stream order, so they may share one buffer; two streams never do, so concurrent calls on two
+    streams (of one thread or of several) cannot race on the scratch.  A buffer is allocated while
+    its stream is current, so when it grows the caching allocator hands the old block out again
+    only to work queued after it on that same stream (torch's stream-ordered reuse): a kernel
+    still reading the old scratch is never overwritten."""
 
     def __init__(self):
         self._bufs = {}
@@ -268,13 +277,21 @@ class Workspace:
 
     def get(self, device, nbytes):
         import torch
-        key = (str(device), threading.get_ident())
+        dev = torch.device(device)
+        st = torch.cuda.current_stream(dev)
+        key = (str(dev), st.cuda_stream)
         with self._lock:
             buf = self._bufs.get(key)
             if buf is None or buf.numel() < nbytes:
-                buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+                with torch.cuda.stream(st):
+                    buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
                 self._bufs[key] = buf
             return buf
+
+    def release(self):
+        """Drop every cached buffer (tests; a long-lived process after a large call)."""
+        with self._lock:
+            self._bufs.clear()
 
 
 WORKSPACE = Workspace()

@@ -141,6 +141,12 @@ class Compressor:
         #   row_groups   None | g                   (folds pipelined under the next group's pass)
         self.dither_path = None
         self.row_groups = None
+        # what (not how): the p = 2 norm of standard dithering / QSGD in compressVector —
+        #   "exact"      the correctly rounded norm (default; deterministic on every host)
+        #   "torch_cpu"  the reference's own fp32 value, torch.norm(x, p=2) on a CPU tensor
+        #                (compressors.py:272) in torch's CPU reduction order, bit for bit
+        #                (flc_norm2_torch_cpu; latency-bound: ~ms per row at D = 25 M)
+        self.norm_mode = "exact"
 
     # -- constants -------------------------------------------------------------------------
     def fullName(self):
@@ -319,9 +325,38 @@ class Compressor:
         d = max(x.shape)
         if self.compressorType == CompressorType.IDENTICAL:
             out = x                                                     # alias, like the reference
+        elif self._torch_norm():
+            out = self._encode_gpu(x, pnorm_in=self.torchNorm(x))
         else:
             out = self._encode_gpu(x)
         self._account(d)
+        return out
+
+    def _torch_norm(self):
+        mode = getattr(self, "norm_mode", "exact")
+        if mode not in ("exact", "torch_cpu"):
+            raise ValueError(f"norm_mode must be 'exact' or 'torch_cpu' (got {mode!r})")
+        if mode == "exact" or self.compressorType != CompressorType.STANDARD_DITHERING_FP32:
+            return False
+        if self.p == 2:
+            return True
+        if self.p == math.inf:
+            return False                       # max |x_j|: no rounding, every order gives it
+        raise NotImplementedError(f"norm_mode='torch_cpu' restates torch's p=2 reduction only (p={self.p})")
+
+    def torchNorm(self, x):
+        """torch.norm(x, p=2) as the reference's CPU fp32 path computes it (compressors.py:272),
+        bit for bit, on the GPU (flc_norm2_torch_cpu): a [1] fp32 device tensor."""
+        if x.dtype != torch.float32:
+            raise TypeError(f"flcodec encodes fp32 only (got {x.dtype})")
+        dev = _gpu_device(x)
+        xd = x.reshape(-1).to(device=dev).contiguous()
+        out = torch.empty(1, dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        with torch.cuda.device(dev):
+            rc = lib.flc_norm2_torch_cpu(ctypes.c_void_p(xd.data_ptr()), xd.numel(), 1, xd.numel(),
+                                         ctypes.c_void_p(out.data_ptr()), _lib.stream_ptr(dev))
+        _lib.check(rc, "flc_norm2_torch_cpu")
         return out
 
     def _pattern(self, dev, keep):

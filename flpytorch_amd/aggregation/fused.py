@@ -32,7 +32,7 @@ def _device(device):
 
 
 def select_row_flags(comp: Compressor, n, d, device=None):
-    """Path report of the last TopK call on this thread's workspace (flc_select_row_flags): a
+    """Path report of the last TopK call on the current stream's workspace (flc_select_row_flags): a
     [n] int64 tensor of row state bits — 1 overflow, 2 short list, 4 ties cut on the fast path,
     8 exact path.  Call it right after the UplinkReducer / compressVector call, with its n and d
     (compressVector: n = 1).  Tests use it to assert which path ran."""
@@ -110,6 +110,9 @@ class UplinkReducer:
         """The call on the current stream (allocations, uploads and the launch all on it)."""
         lib = _lib.load()
         dev = self.device
+        if self.comp._torch_norm():
+            raise NotImplementedError("UplinkReducer folds with exactly rounded norms; norm_mode='torch_cpu' "
+                                      "(the reference's CPU norm bits) is served by compressVector")
         prm, keep = self.params()
         pat = _lib.FlcPattern()
         pat.client0 = int(client0)

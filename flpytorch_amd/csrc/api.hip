@@ -109,6 +109,15 @@ extern "C" int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int6
     return sel_row_flags(prm, n, d, d_workspace, ws_bytes, d_flags, (hipStream_t)stream);
 }
 
+extern "C" int flc_norm2_torch_cpu(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* stream) {
+    if (n < 0 || d < 0 || (n > 1 && ld < d) || (n > 0 && (!d_rows || !d_out))) {
+        set_error("flc_norm2_torch_cpu: bad args (n=%lld d=%lld ld=%lld)", (long long)n, (long long)d, (long long)ld);
+        return FLC_ERR_ARG;
+    }
+    if (n == 0) return FLC_OK;
+    return norm_torch_run(d_rows, ld, n, d, d_out, (hipStream_t)stream);
+}
+
 namespace flc {
 int selftest_division(const float* d_b, int nb, unsigned long long* d_bad, hipStream_t st);
 }

@@ -841,4 +841,73 @@ int selftest_division(const float* d_b, int nb, unsigned long long* d_bad, hipSt
     return FLC_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// The fp32 2-norm in torch's CPU reduction order (compressors.py:272 `torch.norm(x, p=2)` on a
+// CPU fp32 tensor; oracle/torch_norm.c restates it and tests/golden/rows.json pins it at D = 25 M):
+// 8 lane accumulators, lane l taking x[8k + l]^2 in order as fused multiply-adds, the 8 lanes
+// summed left to right, the D % 8 tail elements' squares added in order (fused), then the
+// correctly rounded square root.  Each lane's sum is one chain of D / 8 dependent fmas, which
+// no reassociation may shorten: one workgroup per row, wave 0's lanes 0..7 run the chains out
+// of LDS while waves 1..3 stream the row into a double buffer (transposed so that a chain reads
+// 4 consecutive steps per ds_read_b128).  Latency-bound by design (~3 M dependent fmas per
+// chain at D = 25 M): the parity mode of the drop-in, not a fast path.
+// ------------------------------------------------------------------------------------------
+constexpr int TN_CH = 8192;                 // elements per staged chunk
+constexpr int TN_ST = TN_CH / 8 + 4;        // LDS stride of a lane's steps (+4: conflict-free staging)
+
+__global__ __launch_bounds__(256) void k_norm_torch(const float* __restrict__ base, int64_t ld, int64_t d,
+                                                    float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float buf[2][8 * TN_ST];
+    const int t = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    const float* r = base + row * ld;
+    const int64_t m = d - d % 8;                              // the lane accumulators' elements
+    const int64_t nc = (m + TN_CH - 1) / TN_CH;
+    // waves 1..3 stage chunk c (zeros past m: fmaf(0, 0, a) == a for every a, so the padding
+    // leaves the chains' bits unchanged)
+    auto stage = [&](int64_t c) {
+        float* b = buf[c & 1];
+        const int64_t j0 = c * TN_CH;
+        for (int i = t - 64; i < TN_CH; i += 192) {
+            const int64_t j = j0 + i;
+            b[(i & 7) * TN_ST + (i >> 3)] = j < m ? __builtin_nontemporal_load(r + j) : 0.f;
+        }
+    };
+    float acc = 0.f;
+    if (t >= 64 && nc > 0) stage(0);
+    __syncthreads();
+    for (int64_t c = 0; c < nc; ++c) {
+        if (t >= 64) {
+            if (c + 1 < nc) stage(c + 1);
+        } else if (t < 8) {
+            const float4* b4 = reinterpret_cast<const float4*>(buf[c & 1] + t * TN_ST);
+#pragma unroll 8
+            for (int s = 0; s < TN_CH / 32; ++s) {
+                const float4 v = b4[s];
+                acc = fmaf(v.x, v.x, acc);
+                acc = fmaf(v.y, v.y, acc);
+                acc = fmaf(v.z, v.z, acc);
+                acc = fmaf(v.w, v.w, acc);
+            }
+        }
+        __syncthreads();
+    }
+    if (t < 64) {
+        float tot = __shfl(acc, 0, 64);
+        for (int l = 1; l < 8; ++l) tot = tot + __shfl(acc, l, 64);   // buffer[0] + buffer[1] + ...
+        if (t == 0) {
+            for (int64_t k = m; k < d; ++k) tot = fmaf(r[k], r[k], tot);
+            out[row] = (float)sqrt((double)tot);               // RN(sqrt): exact via double
+        }
+    }
+}
+
+int norm_torch_run(const float* x, int64_t ld, int64_t n, int64_t d, float* out, hipStream_t st) {
+    if (n <= 0) return FLC_OK;
+    ProfScope _ps("k_norm_torch", st);
+    hipLaunchKernelGGL(k_norm_torch, dim3((unsigned)n), dim3(256), 0, st, x, ld, d, out);
+    FLC_CHECK_LAUNCH("k_norm_torch");
+    return FLC_OK;
+}
+
 }  // namespace flc

@@ -162,12 +162,16 @@ int shift_run(const flc_codec_params* prm, const flc_pattern* pat, const float* 
               float* pnorm_out, void* ws, size_t ws_bytes, hipStream_t st);
 // Row g's boundary of G row groups whose last group is `lastpct` % of the others' size (the last
 // group's tail is the exposed one): rows [group_row(n, G, g), group_row(n, G, g + 1)).
+// lastpct is clamped to [1, 100]: 0 or less would leave the last group (the one whose fold writes
+// the output) empty, above 100 is the even split.
 inline int64_t group_row(int64_t n, int G, int g, int lastpct) {
+    lastpct = lastpct < 1 ? 1 : lastpct;
     if (G <= 1 || lastpct >= 100) return n * g / G;
     const int64_t unit = 100 * (int64_t)(G - 1) + lastpct;     // group sizes 100, ..., 100, lastpct
     const int64_t cum = g <= G - 1 ? 100 * (int64_t)g : unit;
     return n * cum / unit;
 }
+int norm_torch_run(const float* x, int64_t ld, int64_t n, int64_t d, float* out, hipStream_t st);
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st);

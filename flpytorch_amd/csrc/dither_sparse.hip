@@ -1174,10 +1174,21 @@ __device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r
 #ifndef FLC_DS_MASKLD
 #define FLC_DS_MASKLD 0
 #endif
+#ifndef FLC_DS_RAWRING
+#define FLC_DS_RAWRING 0             // k_ds_accum: raw list loads in the ring, masked where folded
+#endif
 #ifndef FLC_DS_AW
 #define FLC_DS_AW 1                  // waves per fold workgroup (LDS: one 8 KB tile per wave)
 #endif
 constexpr int DS_AW = FLC_DS_AW;
+#ifndef FLC_DS_AWPE
+#define FLC_DS_AWPE 0                // k_ds_accum: minimum waves per SIMD the register allocation targets (0: compiler's choice)
+#endif
+#if FLC_DS_AWPE > 0
+#define FLC_DS_ACCUM_ATTR __attribute__((amdgpu_waves_per_eu(FLC_DS_AWPE)))
+#else
+#define FLC_DS_ACCUM_ATTR
+#endif
 
 // Folds rows [r0, r0 + rn) into the running sums: the first group starts the tiles at -0, the others
 // continue from `part` (the previous group's tiles); the last group resolves untouched columns
@@ -1187,7 +1198,7 @@ constexpr int DS_AW = FLC_DS_AW;
 // The row walk is a ring of AP rows' first 64 entries: row q's slot is refilled with row q + AP
 // as soon as q is folded, so a list load has AP - 1 rows of work in front of it.
 template <bool W, int AP, bool COMPAT>
-__global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
+__global__ __launch_bounds__(64 * DS_AW) FLC_DS_ACCUM_ATTR void k_ds_accum(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int first, int last,
                                                   int64_t d, DsWs ws, const float* __restrict__ levels, int s,
                                                   const float* __restrict__ w, float wt, float* __restrict__ part,
                                                   float* __restrict__ out, UniformSrc us) {
@@ -1263,9 +1274,84 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
             if (q + AP < 64) fetch(cur, q + AP, i0 + q + AP, q % AP);
             else fetch(nxt, q + AP - 64, i0 + q + AP, q % AP);   // q % AP: static once unrolled
         };
+#if FLC_DS_RAWRING
+        // Raw ring: row q's slot holds the first 64 u16 of its region, loaded whatever its count
+        // (rows clamped to the array's last row) and masked with the count where the row is
+        // folded.  The refill address thus needs no row state, and no select sits between a load
+        // and its use: each row waits for its own load only (a static vmcnt(AP - 1)).  (The
+        // previous form masked at the load and took a general path inside the same loop: the
+        // compiler copied the ring at the back-edges and waited for the whole ring there.)
+        const uint16_t* hb = ws.ent16 + h * n * DS_HCAP + lane;
+#pragma unroll
+        for (int q = 0; q < AP; ++q) ra[q] = hb[min(r0 + q, n - 1) * DS_HCAP];
+        int64_t b = 0;
+        // 64-row batches (the last one may be partial: its rows past the end have count 0) until
+        // one holds a dense row; from there the rows go one at a time below
+        for (; b < nb; ++b) {
+            const int64_t i0 = r0 + b * 64;
+            if (__ballot((cur.mode & DS_DENSE) != 0u) != 0ull) break;
+            nxt = ds_meta(ws, h, n, rend, i0 + 64 + lane, w);
+#pragma unroll 1
+            for (int qb = 0; qb < 64; qb += AP) {
+#pragma unroll
+                for (int u = 0; u < AP; ++u) {
+                    const int q = qb + u;
+                    float pn, wi;
+                    row_state(cur, q, pn, wi);
+                    const uint32_t cnt = __builtin_amdgcn_readlane(cur.cnt, q);
+                    const uint32_t a = (uint32_t)lane < cnt ? ra[u] : NONE;
+                    const float e = value(a, pn);
+                    if (a != NONE) add(a & (HCHUNK - 1), W ? wi * e : e);
+                    if (__builtin_expect(cnt > 64u, 0)) {             // rare: the rest of a long list
+                        const int64_t row = i0 + q;
+                        for (uint32_t k = 64u + lane; k < cnt; k += 64) {
+                            const uint32_t en = ws.ent16[(h * n + row) * DS_HCAP + k];
+                            const float ev = value(en, pn);
+                            add(en & (HCHUNK - 1), W ? wi * ev : ev);
+                        }
+                    }
+                    ra[u] = hb[min(i0 + q + AP, n - 1) * DS_HCAP];
+                }
+            }
+            cur = nxt;
+        }
+        // rows from the batch with a dense row on, one at a time (rare: a row outside its sample's
+        // norm bounds, an overflowed item, a non-finite row or weight)
+        for (int64_t row = r0 + b * 64; row < rend; ++row) {
+            const uint32_t mode = ws.flags[row];
+            const float pn = ws.pn[row], wi = W ? w[row] : 1.f;
+            if (mode & DS_DENSE) {
+                // dense row: every element of the half chunk, coalesced
+                DsRow rr;
+                rr.n = pn;
+                rr.rn = ws.rpn[row];
+                const uint32_t rk = ws.rk[row];
+                rr.rk2 = rk ^ 0x27D4EB2Fu;
+                rr.fast = (mode & DS_FAST) != 0u;
+                const float* rp = rows.row(row) + hbase;
+                for (int k = 0; k < HCHUNK / 64; ++k) {
+                    const uint32_t e = (uint32_t)(k * 64 + lane);
+                    if (e < (uint32_t)len) {
+                        const uint32_t j = hbase + e;
+                        const float ev = COMPAT ? ds_encode<true>(rp[e], j, 0u, us.u[row * us.uld + j], rr, tab, s, sf)
+                                                : ds_encode<false>(rp[e], j, ds_hi8(j, rk), 0.0, rr, tab, s, sf);
+                        add(e, W ? wi * ev : ev);
+                    }
+                }
+            } else {
+                const uint32_t cnt = ws.tabs[h * n + row].y + ws.cntr[h * n + row];
+                for (uint32_t k = lane; k < cnt; k += 64) {
+                    const uint32_t en = ws.ent16[(h * n + row) * DS_HCAP + k];
+                    const float ev = value(en, pn);
+                    add(en & (HCHUNK - 1), W ? wi * ev : ev);
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int q = 0; q < AP; ++q) fetch(cur, q, r0 + q, q);
-        for (int64_t b = 0; b < nb; ++b) {
+        int64_t b = 0;
+        for (; b < nb; ++b) {
             const int64_t i0 = r0 + b * 64;
             nxt = ds_meta(ws, h, n, rend, i0 + 64 + lane, w);
             // rows of this batch that need the general path: dense, or more than 64 entries here
@@ -1344,6 +1430,7 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
             }
             cur = nxt;
         }
+#endif
         if (!last) {
             for (int64_t i = lane; i < len; i += 64) part[hbase + i] = tl[i];
             continue;
@@ -1384,8 +1471,18 @@ __global__ __launch_bounds__(64 * DS_AW) void k_ds_accum(RowSrc rows, int64_t n,
 #ifndef FLC_DS_LASTPCT
 #define FLC_DS_LASTPCT 100           // size of the last QSGD row group in % of the others (its tail is exposed)
 #endif
+static_assert(FLC_DS_LASTPCT >= 1 && FLC_DS_LASTPCT <= 100, "FLC_DS_LASTPCT: the last row group is 1..100 % of the others");
 #ifndef FLC_DS_RG_SIDE
 #define FLC_DS_RG_SIDE 1             // row groups: norm + resolve on the side stream too
+#endif
+#ifndef FLC_DS_RESGRID
+#define FLC_DS_RESGRID 0             // k_ds_filter: a resident grid (one round of blocks, grid-stride items)
+#endif
+#ifndef FLC_DS_SIDE_FOLD_WG
+#define FLC_DS_SIDE_FOLD_WG 0        // a non-last row group's fold (beside the next filter): grid cap, 0 = one per half
+#endif
+#ifndef FLC_DS_SIDE_RES_WG
+#define FLC_DS_SIDE_RES_WG 0         // a non-last row group's resolve: grid cap, 0 = one wave per 64 items
 #endif
 #ifndef FLC_DS_PROBE_DEF
 #define FLC_DS_PROBE_DEF 0           // A/B variant builds only (a probe's outputs are NOT valid)
@@ -1501,7 +1598,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     const UniformSrc us{compat ? pat->d_uniforms : nullptr, (pat && pat->uniforms_ld) ? pat->uniforms_ld : d};
 
     hipEvent_t filt_ev = nullptr;
-    auto filter = [&](int64_t r0, int64_t rn, hipStream_t s2 = nullptr) -> int {
+    auto filter = [&](int64_t r0, int64_t rn, hipStream_t s2 = nullptr, bool beside = false) -> int {
         // s2: the row group's norm / resolve go to this stream (after an event on st), under the
         // next group's filter
         auto kern = compat ? (v.cring == 8 ? k_ds_filter<8, DS_GCAP, 0, true> : k_ds_filter<DS_RINGC, DS_GCAP, 0, true>)
@@ -1510,17 +1607,21 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
                   : v.probe == 5 ? k_ds_filter<16, DS_GCAP, 5> : v.probe == 6 ? k_ds_filter<16, DS_GCAP, 6>
                   : FLC_DS_V2 ? k_ds_filter2<16, FLC_DS2_CAP> : k_ds_filter<16, DS_GCAP>;
         int gw = (int)std::max<int64_t>(1, std::min<int64_t>((rn * ws.G + 3) / 4, 32768));
-        if (v.resident || (K > 1 && v.gridpct < 100)) {
-            int per = 0, dev = 0, cus = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) == hipSuccess && per > 0)
-                gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
-        }
         // row groups (s2: the group's tail runs beside the next group's filter): the filter's
         // blocks reserve FLC_DS_LDSPAD more bytes of LDS, so one block fewer fits a CU and the
         // side stream's tail kernels find room without waiting for a filter block to retire
         const size_t pad = s2 ? (size_t)FLC_DS_LDSPAD : 0u;
+        if (FLC_DS_RESGRID || v.resident || (K > 1 && v.gridpct < 100)) {
+            // resident grid: exactly the blocks that fit the chip at once (the LDS pad counted),
+            // each walking its items grid-stride, so no block retires before the end — no partial
+            // last round of blocks, and the side stream's kernels get only the room left beside
+            // the filter instead of every slot a retiring filter block frees
+            int per = 0, dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, pad) == hipSuccess && per > 0)
+                gw = std::min(gw, std::max(1, per * cus * (K > 1 ? v.gridpct : 100) / 100));
+        }
         { ProfScope _ps("k_ds_filter", st);
         hipLaunchKernelGGL(kern, dim3(gw), dim3(256), pad, st, rows, n, r0, rn, std::min<int64_t>(v.rb, rn), d, ws, us); }
         FLC_CHECK_LAUNCH("k_ds_filter");
@@ -1532,15 +1633,19 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         }
         hipLaunchKernelGGL(k_ds_final, dim3((unsigned)((rn + 3) / 4)), dim3(256), 0, sr, r0, rn, ws, w, pnorm_out);
         FLC_CHECK_LAUNCH("k_ds_final");
-        const int rb = (int)std::max<int64_t>(1, std::min<int64_t>(((rn + 63) / 64 * ws.G + 3) / 4, 8192));
+        int rb = (int)std::max<int64_t>(1, std::min<int64_t>(((rn + 63) / 64 * ws.G + 3) / 4, 8192));
+        // beside the next group's filter: a bounded grid (grid-stride), so the side kernel holds a
+        // fixed share of the CUs instead of taking every slot a retiring filter block frees
+        if (beside && FLC_DS_SIDE_RES_WG > 0) rb = std::min(rb, FLC_DS_SIDE_RES_WG);
         { ProfScope _ps("k_ds_resolve", sr);
         hipLaunchKernelGGL(compat ? k_ds_resolve<true> : k_ds_resolve<false>, dim3(rb), dim3(256), 0, sr, n, r0, rn, ws,
                            prm->d_levels, prm->s, us); }
         FLC_CHECK_LAUNCH("k_ds_resolve");
         return FLC_OK;
     };
-    auto accum = [&](int64_t r0, int64_t rn, int first, int last, hipStream_t s2) -> int {
-        const int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + DS_AW - 1) / DS_AW, 32768));
+    auto accum = [&](int64_t r0, int64_t rn, int first, int last, hipStream_t s2, bool beside = false) -> int {
+        int ab = (int)std::max<int64_t>(1, std::min<int64_t>((H + DS_AW - 1) / DS_AW, 32768));
+        if (beside && FLC_DS_SIDE_FOLD_WG > 0) ab = std::min(ab, FLC_DS_SIDE_FOLD_WG);
         ProfScope _ps("k_ds_accum", s2);
         auto kern = w ? (compat ? k_ds_accum<true, DS_AP, true> : k_ds_accum<true, DS_AP, false>)
                       : (compat ? k_ds_accum<false, DS_AP, true> : k_ds_accum<false, DS_AP, false>);
@@ -1598,7 +1703,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
             // the group's whole tail (norm, resolve, fold) on the side stream, under the next
             // group's filter
             filt_ev = cx.ev[g];
-            rc = filter(r0, r1 - r0, cx.side);
+            rc = filter(r0, r1 - r0, cx.side, g < K - 1);
         } else {
             rc = filter(r0, r1 - r0);
             if (!rc) {
@@ -1607,7 +1712,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
             }
         }
         if (rc) return rc;
-        rc = accum(r0, r1 - r0, g == 0, g == K - 1, cx.side);
+        rc = accum(r0, r1 - r0, g == 0, g == K - 1, cx.side, g < K - 1);
         if (rc) return rc;
     }
     FLC_CHECK_HIP(hipEventRecord(cx.ev[K], cx.side));

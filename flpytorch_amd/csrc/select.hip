@@ -1165,9 +1165,16 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
         const uint32_t thr = prefix;                                    // the K-th key; krem ties admitted
         uint32_t* oi = ws.ent_idx + row * ws.cap;
         float* ov = ws.ent_val + row * ws.cap;
-        uint32_t base = 0, tie_run = 0;
-        for (int64_t c = 0; c < C; ++c) {
-            const int64_t j0 = c * CHUNK + (int64_t)t * 4;
+        // a chunk is CHUNK / (NT * 4) sub-blocks of NT * 4 columns (1 for NT = 1024, 2 / 4 for the
+        // 512 / 256-thread selects), walked in index order with base and tie_run carried across them
+        static_assert(CHUNK % (NT * 4) == 0, "exact_row: NT * 4 must divide CHUNK");
+        constexpr int SUBS = CHUNK / (NT * 4);
+        uint32_t base = 0, tie_run = 0, cbase = 0;
+        for (int64_t cs = 0; cs < C * SUBS; ++cs) {
+            const int64_t c = cs / SUBS;
+            const int sb = (int)(cs % SUBS);
+            if (sb == 0) cbase = base;
+            const int64_t j0 = c * CHUNK + (int64_t)sb * (NT * 4) + (int64_t)t * 4;
             float v[4];
             if (VEC && j0 + 3 < d) {
                 const float4 q = ld_row4(reinterpret_cast<const float4*>(r + j0));
@@ -1201,9 +1208,9 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if (adm[q]) { oi[pos] = (uint32_t)(j0 + q); ov[pos] = v[q]; ++pos; }
-            if (t == 0) ws.tab[c * n + row] = make_uint2(base, atot);
             base += atot;
             tie_run += etot;
+            if (sb == SUBS - 1 && t == 0) ws.tab[c * n + row] = make_uint2(cbase, base - cbase);
         }
         if (t == 0) {
             ws.thr[row] = thr;
@@ -2386,6 +2393,7 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
 #ifndef FLC_TK_LASTPCT
 #define FLC_TK_LASTPCT 100            // size of the last TopK row group in % of the others (its tail is exposed)
 #endif
+static_assert(FLC_TK_LASTPCT >= 1 && FLC_TK_LASTPCT <= 100, "FLC_TK_LASTPCT: the last row group is 1..100 % of the others");
 #ifndef FLC_TK_LAST_TS
 #define FLC_TK_LAST_TS 4096           // the exposed last group fold's tile (columns per wave)
 #endif

@@ -282,6 +282,15 @@ size_t flc_device_randk_counts_workspace_size(int64_t n, int64_t d);
 int flc_device_randk_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d, int64_t k, uint32_t* d_counts,
                             void* d_ws, size_t ws_bytes, void* stream);
 
+/* The fp32 2-norm of each of n rows (row i at d_rows + i*ld) in torch's CPU reduction order —
+ * the norm the reference computes, compressors.py:272 `torch.norm(x, p=2)` on a CPU fp32
+ * tensor, bit for bit (torch 2.10: 8 lane accumulators of fused multiply-adds summed left to
+ * right, the D % 8 tail added in order, then the correctly rounded sqrt; oracle/torch_norm.c,
+ * pinned by tests/golden/rows.json at D = 25 M).  Not exactly rounded (14 616 ulp below the exact
+ * norm at D = 25 M); hand it to flc_encode's d_pnorm_in to get the reference's dithering bits.
+ * Each row is D / 8 dependent fmas per lane: latency-bound (a parity mode, ~ms at D = 25 M). */
+int flc_norm2_torch_cpu(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* stream);
+
 /* Self-test of the exact fast fp32 division the dithering kernels use: for each of the n
  * device divisors, every float numerator in [2^-80, 2^80] is divided both ways and the
  * mismatches are written to d_mismatches[n] (device).  Must be all zero. */

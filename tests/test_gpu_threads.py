@@ -61,3 +61,52 @@ def test_concurrent_threads_distinct_streams():
         else:
             assert np.array_equal(out.cpu().numpy().view(np.uint32), want[i].cpu().numpy().view(np.uint32)), spec
             assert np.array_equal(one.cpu().numpy().view(np.uint32), want_one[i].cpu().numpy().view(np.uint32)), spec
+
+
+def test_one_thread_two_streams_interleaved():
+    """ONE host thread queues TopK on stream A and QSGD on stream B back to back,
+    several times, without synchronising in between, with row sizes that make the second call's
+    workspace grow.  The scratch is per stream (_lib.WORKSPACE keyed by (device, stream)), so the
+    two calls cannot share or free each other's workspace; each result is bit-exact vs the oracle
+    (TopK: oracle encode + sequential fold; QSGD: compat uniforms, oracle encode)."""
+    assert torch.cuda.is_available()
+    from flpytorch_amd import aggregation as ag
+    from oracle import codecs as oc
+    from oracle.rng import OracleRandomState
+
+    n = 4
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for d in (50_003, 300_007):                      # the second size grows both streams' scratch
+        rng = np.random.default_rng([d, 11])
+        rows = rng.standard_normal((n, d)).astype(np.float32)
+        rt = torch.from_numpy(rows).cuda()
+        want = {}
+        uni = None
+        for spec in ("topk:1%", "qsgd:127"):
+            rs = OracleRandomState(7)
+            enc, us = [], []
+            for i in range(n):
+                o = oc.OracleCompressor(spec, d)
+                o.generate(rs)
+                rs.randint31()
+                enc.append(o.compress(rows[i]))
+                if o.type == oc.STD_DITHERING:
+                    us.append(o.testp)
+            want[spec] = oc.reduce_plain(enc)
+            if us:
+                uni = torch.from_numpy(np.stack(us)).cuda()
+        torch.cuda.synchronize()
+        red_t = ag.UplinkReducer(ag.initCompressor("topk:1%", d))
+        red_q = ag.UplinkReducer(ag.initCompressor("qsgd:127", d))
+        outs = []
+        for _ in range(3):
+            with torch.cuda.stream(sa):
+                ot = red_t(rt, stream=sa)
+            with torch.cuda.stream(sb):
+                oq = red_q(rt, uniforms=uni, stream=sb)
+            outs.append((ot, oq))
+        sa.synchronize()
+        sb.synchronize()
+        for ot, oq in outs:
+            assert np.array_equal(ot.cpu().numpy().view(np.uint32), want["topk:1%"].view(np.uint32))
+            assert np.array_equal(oq.cpu().numpy().view(np.uint32), want["qsgd:127"].view(np.uint32))

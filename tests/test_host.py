@@ -356,3 +356,28 @@ def test_torch_cpu_time_uplink_phases():
     from oracle.torch_cpu import time_uplink
     r = time_uplink(["randk:1%", "topk:1%", "qsgd:4"], 10007, budget_s=0.01)
     assert r["clients"] >= 2 and all(r[k] >= 0 for k in ("pattern_s", "compress_s", "fold_s"))
+
+
+def test_torch_norm_oracle_vs_torch_on_this_host():
+    """oracle/torch_norm.c restates torch.norm(x, p=2) for CPU fp32 tensors (compressors.py:272):
+    bit-equal to torch itself here for lengths around the 8-lane accumulator and its tail, and
+    mixed magnitudes.  (The GPU kernel flc_norm2_torch_cpu is checked against this restatement in
+    tests/test_gpu_norm_torch.py; the reference's recorded norms pin both in
+    tests/test_oracle_golden.py.)"""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from oracle import rng
+    rng._load()
+    lib = ctypes.CDLL(rng._LIB_PATH)
+    lib.orc_torch_norm2.restype = ctypes.c_float
+    lib.orc_torch_norm2.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    g = np.random.default_rng(2025)
+    for d in [1, 3, 7, 8, 9, 15, 16, 17, 100, 1001, 4099, 65543, 300_007]:
+        for _ in range(3):
+            x = (g.standard_normal(d) * 10.0 ** g.uniform(-3, 3, d)).astype(np.float32)
+            want = np.float32(torch.norm(torch.from_numpy(x), p=2).item())
+            got = np.float32(lib.orc_torch_norm2(x.ctypes.data, d))
+            assert got.view(np.uint32) == want.view(np.uint32), (d, got, want)
