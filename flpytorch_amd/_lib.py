@@ -21,6 +21,8 @@ FLC_NORM_LINF, FLC_NORM_L1, FLC_NORM_L2 = 0, 1, 2
 FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
 # execution hints (flc_codec_params.flags): how, never what — every choice gives the same bits
 FLC_PATH_AUTO, FLC_PATH_SPARSE, FLC_PATH_DENSE = 0, 1, 2
+FLC_TIE_LOWEST, FLC_TIE_HIGHEST = 0, 1
+ABI_VERSION = 101
 
 
 def FLC_ROW_GROUPS(g):
@@ -56,6 +58,7 @@ class FlcCodecParams(ctypes.Structure):
         ("randk_scale", ctypes.c_float),
         ("d_levels", ctypes.c_void_p),
         ("seed", ctypes.c_uint64),
+        ("tie", ctypes.c_int32),
     ]
 
 

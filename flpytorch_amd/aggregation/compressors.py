@@ -147,6 +147,10 @@ class Compressor:
         #                (compressors.py:272) in torch's CPU reduction order, bit for bit
         #                (flc_norm2_torch_cpu; latency-bound: ~ms per row at D = 25 M)
         self.norm_mode = "exact"
+        # what: TopK's choice among entries tied at the K-th magnitude when fewer places are left
+        # than ties (compressors.py:332 leaves it to torch.topk) — "lowest" indices (default: the
+        # order torch.topk's CPU kernel gave on the reference's rows) or "highest" (flc_codec_params.tie)
+        self.tie_policy = "lowest"
 
     # -- constants -------------------------------------------------------------------------
     def fullName(self):
@@ -297,6 +301,10 @@ class Compressor:
         prm.flags = flags[getattr(self, "dither_path", None)]
         if getattr(self, "row_groups", None):
             prm.flags |= _lib.FLC_ROW_GROUPS(self.row_groups)
+        ties = {"lowest": _lib.FLC_TIE_LOWEST, "highest": _lib.FLC_TIE_HIGHEST}
+        if getattr(self, "tie_policy", "lowest") not in ties:
+            raise ValueError(f"tie_policy must be 'lowest' or 'highest' (got {self.tie_policy!r})")
+        prm.tie = ties[getattr(self, "tie_policy", "lowest")]
         return prm, keep
 
     def _need_to_send(self, d):

@@ -59,12 +59,20 @@ void prof_record(const char* name, hipStream_t st, bool begin) {
 
 static bool is_sel(int codec) { return codec == FLC_TOPK || codec == FLC_RANDK; }
 static bool known(int codec) { return codec >= FLC_IDENT && codec <= FLC_RANK_K; }
+// host-side check of the fields that choose WHAT is computed (before any device argument)
+static int bad_params(const flc_codec_params* prm, const char* what) {
+    if (prm->codec == FLC_TOPK && prm->tie != FLC_TIE_LOWEST && prm->tie != FLC_TIE_HIGHEST) {
+        set_error("%s: unknown TopK tie rule %d (FLC_TIE_LOWEST / FLC_TIE_HIGHEST)", what, (int)prm->tie);
+        return FLC_ERR_ARG;
+    }
+    return FLC_OK;
+}
 
 }  // namespace flc
 
 using namespace flc;
 
-extern "C" int flc_version(void) { return 100; }
+extern "C" int flc_version(void) { return 101; }   // 1.01: flc_codec_params.tie, flc_norm2_torch_cpu
 
 #ifndef FLC_SRC_HASH
 #define FLC_SRC_HASH "unknown"
@@ -182,6 +190,7 @@ extern "C" int flc_encode(const flc_codec_params* prm, const flc_pattern* pat, c
                           const float* d_pnorm_in, float* d_pnorm_out, float* d_out, void* d_ws, size_t ws_bytes,
                           void* stream) {
     if (!prm || !known(prm->codec)) { set_error("flc_encode: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (int rc = bad_params(prm, "flc_encode")) return rc;
     if (d < 0 || (d > 0 && (!d_x || !d_out))) { set_error("flc_encode: bad x/out/d"); return FLC_ERR_ARG; }
     return encode_row(prm, pat, d_x, d, d_pnorm_in, d_pnorm_out, d_out, d_ws, ws_bytes, (hipStream_t)stream);
 }
@@ -196,6 +205,7 @@ extern "C" int flc_encode_shift(const flc_codec_params* prm, const flc_pattern* 
                                 float shift_alpha, const float* d_shift_in, float* d_shift_out, float* d_pnorm_out,
                                 void* d_ws, size_t ws_bytes, void* stream) {
     if (!prm || !known(prm->codec)) { set_error("flc_encode_shift: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (int rc = bad_params(prm, "flc_encode_shift")) return rc;
     if (d < 0) { set_error("flc_encode_shift: d < 0"); return FLC_ERR_ARG; }
     if (d > 0 && (!d_a || !d_b)) { set_error("flc_encode_shift: need a and b"); return FLC_ERR_ARG; }
     if (d > 0 && !d_msg && !d_shift_out) { set_error("flc_encode_shift: nothing to write (msg and shift_out null)"); return FLC_ERR_ARG; }
@@ -229,6 +239,7 @@ extern "C" size_t flc_pack_workspace_size(const flc_codec_params* prm, int64_t d
 extern "C" int flc_pack(const flc_codec_params* prm, const flc_pattern* pat, const float* d_x, int64_t d,
                         void* d_payload, void* d_ws, size_t ws_bytes, void* stream) {
     if (!prm || !known(prm->codec)) { set_error("flc_pack: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (int rc = bad_params(prm, "flc_pack")) return rc;
     if (d < 0 || !d_payload || (d > 0 && !d_x)) { set_error("flc_pack: bad x/payload/d"); return FLC_ERR_ARG; }
     return pack_run(prm, pat, d_x, d, (char*)d_payload, d_ws, ws_bytes, (hipStream_t)stream);
 }
@@ -263,6 +274,7 @@ extern "C" int flc_encode_reduce(const flc_codec_params* prm, const flc_pattern*
                                  const float* const* d_row_ptrs, int64_t n, int64_t d, const float* d_w, float w_total,
                                  float* d_pnorms_out, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
     if (!prm || !known(prm->codec)) { set_error("flc_encode_reduce: unknown codec"); return FLC_ERR_UNSUPPORTED; }
+    if (int rc = bad_params(prm, "flc_encode_reduce")) return rc;
     if (n < 0 || d < 0 || (d > 0 && !d_out)) { set_error("flc_encode_reduce: bad n/d/out"); return FLC_ERR_ARG; }
     if (n > FLC_MAX_ROWS) {   // per-row kernels index rows by blockIdx.y
         set_error("flc_encode_reduce: n=%lld rows, at most %d per call (fold larger rounds as partials)", (long long)n,

@@ -64,7 +64,8 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* prefix;     // [N] radix-select state
     uint32_t* krem;       // [N]
     uint32_t* tieprefix;  // [C][N] ties (key == thr) in chunks before c   (exact path only)
-    uint32_t* tiecut;     // [N] fast path, F_TIES: largest element index admitted among key == thr
+    uint32_t* tiecut;     // [N] fast path, F_TIES: the last index admitted among key == thr (tie_pref order);
+                          // rows selected by k_radix_select<FULLROW> (dense K): the count of keys == thr
     uint32_t* hist;       // [N][HBINS]
     uint32_t* worklist;   // [N] rows on the exact path
     uint32_t* nwork;      // [1]
@@ -76,7 +77,15 @@ struct SelWs {            // carved from the caller workspace
     uint32_t* zm;         // [C][CHUNK / 32] k_chunk_accum (one-wave blocks): a fold job's kept-column mask
     float* part;          // [D] TopK row-group folds: the running tiles carried from one group to the next
     int64_t cap;
+    uint32_t tie_hi;      // TopK ties at the K-th key: 0 the lowest indices are kept (default), 1 the highest
 };
+
+// Tie order of TopK (flc_codec_params.tie): tie_pref(ix) is larger for the index kept first among
+// equal magnitudes — ~ix for the lowest-index rule (the oracle's, torch.topk's CPU order on the
+// reference's rows), ix for the highest-index rule.  A row's tie cut is the last kept tie's index:
+// a tie is admitted iff tie_pref(ix) >= tie_pref(cut); tie_all(ws) is the cut that admits every tie.
+__device__ __host__ inline uint32_t tie_pref(uint32_t ix, uint32_t hi) { return hi ? ix : ~ix; }
+__device__ __host__ inline uint32_t tie_all(uint32_t hi) { return hi ? 0u : 0xFFFFFFFFu; }
 
 
 // ------------------------------------------------------------------------------------------
@@ -372,7 +381,7 @@ __device__ void cand_select_row(int64_t row, int64_t K, SelWs ws, uint32_t* h, u
             for (uint32_t a = threadIdx.x; a < m; a += NT) {
                 const uint32_t ia = tix[a];
                 uint32_t rank = 0;
-                for (uint32_t b = 0; b < m; ++b) rank += tix[b] < ia ? 1u : 0u;
+                for (uint32_t b = 0; b < m; ++b) rank += tie_pref(tix[b], ws.tie_hi) > tie_pref(ia, ws.tie_hi) ? 1u : 0u;
                 if (rank == krem - 1) ws.tiecut[row] = ia;              // indices are distinct
             }
         }
@@ -462,7 +471,7 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws, int fina
             const uint32_t key = mag_key(sv[e]);
             if (((key - T) >> sh) == prefix) {
                 const uint32_t slot = atomicAdd(&scratch[0], 1u);
-                if (slot < (uint32_t)CS_LCAP) lst[slot] = ((uint64_t)key << 32) | (uint64_t)(~si[e]);
+                if (slot < (uint32_t)CS_LCAP) lst[slot] = ((uint64_t)key << 32) | (uint64_t)tie_pref(si[e], ws.tie_hi);
             }
         }
         __syncthreads();
@@ -495,7 +504,7 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws, int fina
                 const uint64_t me = lst[i];
                 uint32_t rank = 0;
                 for (uint32_t j = 0; j < mm; ++j) rank += lst[j] > me ? 1u : 0u;
-                if (rank == krem - 1u) { scratch[0] = (uint32_t)(me >> 32); scratch[1] = ~(uint32_t)me; }
+                if (rank == krem - 1u) { scratch[0] = (uint32_t)(me >> 32); scratch[1] = tie_pref((uint32_t)me, ws.tie_hi); }
             }
         __syncthreads();
         const uint32_t kth = scratch[0];
@@ -610,7 +619,7 @@ __global__ __launch_bounds__(CS_NT) void k_cs_pass(int64_t K, SelWs ws, int fina
             for (uint32_t a = threadIdx.x; a < m; a += CS_NT) {
                 const uint32_t ia = tix[a];
                 uint32_t rank = 0;
-                for (uint32_t bb = 0; bb < m; ++bb) rank += tix[bb] < ia ? 1u : 0u;
+                for (uint32_t bb = 0; bb < m; ++bb) rank += tie_pref(tix[bb], ws.tie_hi) > tie_pref(ia, ws.tie_hi) ? 1u : 0u;
                 if (rank == nk - 1u) ws.tiecut[row] = ia;                // indices are distinct
             }
     }
@@ -671,8 +680,15 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
                 for (int q = 0; q < 4; ++q) v[t][q] = (j + q < d) ? r[j + q] : 0.f;
             }
         }
-        uint32_t tie_base = 0, tie_need = ALL;
-        if (EXACT) { tie_base = ws.tieprefix[c * n + row]; tie_need = ws.krem[row]; }
+        // ties (key == T) admitted: tie ranks [tie_from, tie_need) in index order — the first krem
+        // (lowest-index rule) or the last krem of the row's tot (highest-index rule; k_radix_select
+        // left tot in tiecut)
+        uint32_t tie_base = 0, tie_need = ALL, tie_from = 0;
+        if (EXACT) {
+            tie_base = ws.tieprefix[c * n + row];
+            tie_need = ws.krem[row];
+            if (ws.tie_hi) { const uint32_t tot = ws.tiecut[row]; tie_from = tot - tie_need; tie_need = tot; }
+        }
         // pass 1: count
         uint32_t cnt = 0;
         uint32_t tie_run = tie_base;
@@ -696,7 +712,7 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
                 uint32_t inlane = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if (eq[q]) gt[q] = (tie_run + before + inlane) < tie_need;
+                    if (eq[q]) { const uint32_t tr = tie_run + before + inlane; gt[q] = tr >= tie_from && tr < tie_need; }
                     inlane += eq[q] ? 1u : 0u;
                 }
                 tie_run += __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
@@ -739,7 +755,7 @@ __global__ __launch_bounds__(256) void k_topk_filter(RowSrc rows, int64_t n, int
                 uint32_t inlane = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if (eq[q]) gt[q] = (tie_run + before + inlane) < tie_need;
+                    if (eq[q]) { const uint32_t tr = tie_run + before + inlane; gt[q] = tr >= tie_from && tr < tie_need; }
                     inlane += eq[q] ? 1u : 0u;
                 }
                 tie_run += __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
@@ -1057,6 +1073,7 @@ __global__ __launch_bounds__(256) void k_radix_select(int64_t n, int p, int64_t 
             ws.krem[row] = k - above;
             if (p == 2) {
                 ws.thr[row] = ws.prefix[row];
+                if (FULLROW) ws.tiecut[row] = ties_here;                  // the row's keys == thr (tie order)
                 if (ties_here > k - above) ws.flags[row] |= (FULLROW ? F_TIES | F_EXACT : F_TIES);
                 else if (FULLROW) ws.flags[row] |= F_EXACT;
             }
@@ -1129,7 +1146,7 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
     const int64_t C = nchunks(d);
     {
         const float* r = rows.row(row);
-        uint32_t prefix = 0, krem = (uint32_t)K;
+        uint32_t prefix = 0, krem = (uint32_t)K, ties_tot = 0;
         for (int p = 0; p < 3; ++p) {
             for (int i = t; i < HBINS; i += NT) h[i] = 0;
             __syncthreads();
@@ -1160,9 +1177,12 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
             hist_find(h, krem, bin, above, scratch);
             prefix = (prefix << pass_bits(p)) | bin;                   // p == 0: prefix is 0
             krem -= above;
+            if (p == 2) ties_tot = h[bin];                              // the row's keys == thr
             __syncthreads();
         }
         const uint32_t thr = prefix;                                    // the K-th key; krem ties admitted
+        // tie ranks admitted in index order: [0, krem) (lowest-index rule) or [tot - krem, tot)
+        const uint32_t tie_from = ws.tie_hi ? ties_tot - krem : 0u, tie_to = ws.tie_hi ? ties_tot : krem;
         uint32_t* oi = ws.ent_idx + row * ws.cap;
         float* ov = ws.ent_val + row * ws.cap;
         // a chunk is CHUNK / (NT * 4) sub-blocks of NT * 4 columns (1 for NT = 1024, 2 / 4 for the
@@ -1199,7 +1219,7 @@ __device__ void exact_row(RowSrc rows, int64_t n, int64_t row, int64_t d, int64_
             bool adm[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                adm[q] = gt[q] || (eq[q] && erank < krem);
+                adm[q] = gt[q] || (eq[q] && erank >= tie_from && erank < tie_to);
                 erank += eq[q] ? 1u : 0u;
                 na += adm[q] ? 1u : 0u;
             }
@@ -1564,20 +1584,20 @@ constexpr int AP = FLC_CA_AP;              // rows of entry lists in flight
 
 struct RowMeta {
     uint2 te;          // (offset, count) of the row's list in this chunk
-    uint32_t thr, cut, mode;
+    uint32_t thr, cut, mode;   // cut: tie_pref of the row's tie cut (0 admits every tie)
     float w;
 };
 
 __device__ inline RowMeta load_meta(const SelWs& ws, int64_t c, int64_t n, int64_t r, const float* w, int64_t rend = -1) {
     RowMeta m;
     m.te = make_uint2(0, 0);
-    m.thr = 0; m.cut = 0xFFFFFFFFu; m.mode = 0; m.w = 1.f;
+    m.thr = 0; m.cut = 0u; m.mode = 0; m.w = 1.f;
     if (r < (rend < 0 ? n : rend)) {
         m.te = ws.tab[c * n + r];
         m.thr = ws.thr[r];
         const uint32_t f = ws.flags[r];
         m.mode = (f & F_EXACT) ? 2u : ((f & F_TIES) ? 1u : 0u);
-        if (m.mode == 1u) m.cut = ws.tiecut[r];
+        if (m.mode == 1u) m.cut = tie_pref(ws.tiecut[r], ws.tie_hi);
         if (m.mode == 2u) m.thr = 0u;          // exact list: every entry admitted (key >= 0, cut ~0)
         if (w) m.w = w[r];
     }
@@ -1624,7 +1644,7 @@ __device__ void resolve_neg_zero(float* tl, uint32_t* rm, const SelWs& ws, int64
             const uint32_t ix = ws.ent_idx[r * ws.cap + m.te.x + e];
             const uint32_t key = mag_key(ws.ent_val[r * ws.cap + m.te.x + e]);
             const uint32_t loc = ix - cbase;
-            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut)))
+            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && tie_pref(ix, ws.tie_hi) >= cut)))
                 atomicOr(&rm[loc >> 5], 1u << (loc & 31));
         }
         bool left = false;
@@ -1685,7 +1705,7 @@ __device__ void resolve_neg_zero_g(float* tl, uint32_t* rm, const SelWs& ws, int
             const uint32_t ix = ws.ent_idx[r * ws.cap + m.te.x + e];
             const uint32_t key = mag_key(ws.ent_val[r * ws.cap + m.te.x + e]);
             const uint32_t loc = ix - cbase;
-            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && ix <= cut)))
+            if (loc < (uint32_t)TS && (mode == 2u || key > T || (key == T && tie_pref(ix, ws.tie_hi) >= cut)))
                 atomicOr(&rm[loc >> 5], 1u << (loc & 31));
         }
         __threadfence_block();
@@ -1766,13 +1786,14 @@ __device__ __forceinline__ void chunk_accum_body(int64_t n, int64_t d, SelWs ws,
                 rv[slot][h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dv, lane * 4, h * 256, 0));
             }
         };
-        // admission (key > T, or key == T and ix <= cut; load_meta folds the exact mode into
-        // T = 0, cut = ~0) as ONE 64-bit compare: (key, ~ix) >= (T, ~cut)
+        // admission (key > T, or key == T and tie_pref(ix) >= tie_pref(cut); load_meta folds the
+        // exact mode into T = 0, cut 0) as ONE 64-bit compare: (key, tie_pref(ix)) >= (T, cut)
+        const uint32_t txm = ws.tie_hi ? 0u : 0xFFFFFFFFu;   // tie_pref(ix) = ix ^ txm
         auto fold = [&](uint32_t ix, float vv, uint32_t T, uint32_t cut, uint32_t mode, float wi) {
             (void)mode;
             const uint32_t loc = ix - cbase;                   // ~0 index / other part: loc >= TS
-            const uint64_t a = ((uint64_t)mag_key(vv) << 32) | (uint64_t)(~ix);
-            const uint64_t b = ((uint64_t)T << 32) | (uint64_t)(~cut);
+            const uint64_t a = ((uint64_t)mag_key(vv) << 32) | (uint64_t)(ix ^ txm);
+            const uint64_t b = ((uint64_t)T << 32) | (uint64_t)cut;
             if (FLC_CA_PROBE == 1) {                          // cost probe: no tile update
                 if (loc < (uint32_t)TS && a >= b && vv == 1.2345f) tl[0] = vv;
                 return;
@@ -2224,7 +2245,7 @@ __global__ __launch_bounds__(256) void k_randk_scatter_dev(const float* __restri
 __global__ __launch_bounds__(256) void k_assign_scatter(SelWs ws, float* __restrict__ out, int sharded) {
     const uint32_t T = ws.thr[0], f = ws.flags[0];
     const uint32_t mode = (f & F_EXACT) ? 2u : ((f & F_TIES) ? 1u : 0u);
-    const uint32_t cut = mode == 1u ? ws.tiecut[0] : 0xFFFFFFFFu;
+    const uint32_t cut = mode == 1u ? tie_pref(ws.tiecut[0], ws.tie_hi) : 0u;
     // the list: [0, rowcnt) (one reservation counter, or rewritten by the exact path), else the
     // filter's CS_SH shards, block b taking shards b, b + gridDim.x, ...
     const bool shd = sharded && mode != 2u;
@@ -2236,7 +2257,7 @@ __global__ __launch_bounds__(256) void k_assign_scatter(SelWs ws, float* __restr
             const uint32_t ix = ws.ent_idx[o + e];
             const float v = ws.ent_val[o + e];
             const uint32_t key = mag_key(v);
-            if (mode == 2u || key > T || (key == T && ix <= cut)) out[ix] = v;
+            if (mode == 2u || key > T || (key == T && tie_pref(ix, ws.tie_hi) >= cut)) out[ix] = v;
         }
     }
 }
@@ -2259,7 +2280,7 @@ __global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d,
         return;
     }
     const uint32_t T = ws.thr[0], f = ws.flags[0];
-    const uint32_t cut = (f & F_TIES) ? ws.tiecut[0] : 0xFFFFFFFFu;
+    const uint32_t cut = (f & F_TIES) ? tie_pref(ws.tiecut[0], ws.tie_hi) : 0u;
     const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
     for (int sh = (int)blockIdx.x; sh < CS_SH; sh += (int)gridDim.x) {
         const uint32_t cnt = ws.shcnt[sh * RCS];
@@ -2268,7 +2289,7 @@ __global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d,
             const uint32_t ix = ws.ent_idx[o + e];
             const float v = ws.ent_val[o + e];
             const uint32_t key = mag_key(v);
-            if (key > T || (key == T && ix <= cut)) out[ix] = v;
+            if (key > T || (key == T && tie_pref(ix, ws.tie_hi) >= cut)) out[ix] = v;
         }
     }
 }
@@ -2290,6 +2311,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     Carver cv(base);
     const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
     SelWs s;
+    s.tie_hi = 0;
     s.cap = sel_capacity(codec, d, K);
     s.tab = cv.take<uint2>((size_t)C * nn);
     s.ent_idx = cv.take<uint32_t>((size_t)nn * s.cap);
@@ -2585,6 +2607,10 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     carve_sel(nullptr, codec, n, d, K, &need);
     if (ws_bytes < need) { set_error("select: workspace %zu < %zu", ws_bytes, need); return FLC_ERR_WORKSPACE; }
     SelWs ws = carve_sel(wsp, codec, n, d, K, nullptr);
+    if (codec == FLC_TOPK) {
+        if (prm->tie != FLC_TIE_LOWEST && prm->tie != FLC_TIE_HIGHEST) { set_error("topk: unknown tie rule %d", prm->tie); return FLC_ERR_ARG; }
+        ws.tie_hi = prm->tie == FLC_TIE_HIGHEST ? 1u : 0u;
+    }
     const int64_t C = host_chunks(d);
     bool lone_assign = false, gfold = false;
     // TopK, few rows: sharded candidate lists (k_topk_filter_fast) and the spread select (k_cs_pass)

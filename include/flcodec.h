@@ -80,7 +80,15 @@ typedef struct {
     float randk_scale;      /* randk: (float)(D / K) as the reference's fp32 scalar multiply */
     const float* d_levels;  /* dithering: s+1 fp32 levels (Compressor.levelsValues) on device */
     uint64_t seed;          /* device-RNG mode: experiment key of the counter-based generator */
+    int32_t tie;            /* topk: which of the entries tied at the K-th magnitude are kept when
+                               fewer places are left than ties (compressors.py:332 leaves it to
+                               torch.topk): FLC_TIE_LOWEST (0, the lowest indices: torch.topk's CPU
+                               order on the reference's rows, the oracle's rule) or FLC_TIE_HIGHEST.
+                               A result, not a hint: the two rules give different sets on tied rows. */
 } flc_codec_params;
+
+#define FLC_TIE_LOWEST 0
+#define FLC_TIE_HIGHEST 1
 
 /* Patterns: where the randomness of one call comes from (generateCompressPattern, 196-216).
  * Compat mode reproduces the reference's numpy stream bit for bit (host-drawn, uploaded);

@@ -18,10 +18,12 @@ fp32 semantics reproduced (checked against tests/golden/ fixtures from the real 
     (compressors.py:288);  later level intervals overwrite earlier ones (290-291);
   * ``out * sign * pnorm`` is evaluated left to right in fp32 (296);
   * natural dithering returns ``y * sign * pnorm`` — the reference's own bug (326);
-  * torch's CPU ``norm`` sums in an implementation-defined fp32 order (up to hundreds of
-    ulp from the exact value at D ~ 1e6); the oracle computes the norm exactly (float64
-    accumulation, one rounding) unless the caller passes the reference's value.
-  * TopK ties at the K-th magnitude are broken by lowest index (torch leaves it unspecified).
+  * torch's CPU ``norm`` sums in its own fp32 order (14 616 ulp from the exact value at
+    D = 25 M); the oracle computes the norm exactly (float64 accumulation, one rounding) unless
+    the caller passes a value — the reference's, or oracle/torch_norm.c's restatement of torch's
+    order (the library's norm_mode="torch_cpu").
+  * TopK ties at the K-th magnitude are broken by lowest index (torch leaves it unspecified);
+    ``tie = "highest"`` keeps the highest indices instead (the library's FLC_TIE_HIGHEST).
 """
 import math
 
@@ -61,6 +63,7 @@ class OracleCompressor:
         self.really_need_to_send_components = 0
         self.last_input_advance = 0
         self.last_need_to_send_advance = 0
+        self.tie = "lowest"          # TopK tie rule (the library's flc_codec_params.tie)
 
         def kspec(arg):
             if arg.find("%") == -1:
@@ -193,7 +196,7 @@ class OracleCompressor:
                 need = 1.0 + d * (1.0 + math.ceil(math.log2(self.s))) / 32.0
             elif t == TOPK:
                 out = np.zeros_like(x)
-                ind = topk_indices(x, self.K)
+                ind = topk_indices(x, self.K, self.tie)
                 out[ind] = x[ind]
                 need = self.K
             elif t == RANK_K:                         # compressors.py:336-364
@@ -239,17 +242,19 @@ def topk_keys(x):
     return (np.asarray(x, dtype=_F32).view(np.uint32) & np.uint32(0x7FFFFFFF))
 
 
-def topk_indices(x, K):
+def topk_indices(x, K, tie="lowest"):
     """Indices of the K largest |x|, ties at the K-th magnitude broken by lowest index
-    (compressors.py:330-335 with torch.topk's CPU tie order)."""
+    (compressors.py:330-335 with torch.topk's CPU tie order) or, tie="highest", by highest index
+    (the library's FLC_TIE_HIGHEST)."""
     key = topk_keys(x).astype(np.int64)
-    order = np.lexsort((np.arange(key.size), -key))
+    pos = np.arange(key.size) if tie == "lowest" else -np.arange(key.size)
+    order = np.lexsort((pos, -key))
     return np.sort(order[:K])
 
 
-def topk_indices_fast(x, K):
+def topk_indices_fast(x, K, tie="lowest"):
     """topk_indices by selection instead of a full sort (same set; large rows in the GPU tests):
-    every key above the K-th key, then the lowest-index keys equal to it."""
+    every key above the K-th key, then the lowest- (or highest-) index keys equal to it."""
     key = topk_keys(x)
     K = int(K)
     if K <= 0:
@@ -258,7 +263,8 @@ def topk_indices_fast(x, K):
         return np.arange(key.size, dtype=np.int64)
     kth = np.partition(key, key.size - K)[key.size - K]
     above = np.flatnonzero(key > kth)
-    ties = np.flatnonzero(key == kth)[:K - above.size]
+    eq = np.flatnonzero(key == kth)
+    ties = eq[:K - above.size] if tie == "lowest" else eq[eq.size - (K - above.size):]
     return np.sort(np.concatenate([above, ties])).astype(np.int64)
 
 

@@ -7,7 +7,7 @@
 #include "flcodec.h"
 
 int main(void) {
-    if (flc_version() != 100) { printf("bad version\n"); return 1; }
+    if (flc_version() != 101) { printf("bad version\n"); return 1; }
     flc_codec_params prm;
     memset(&prm, 0, sizeof(prm));
     prm.codec = FLC_TOPK;
@@ -25,6 +25,24 @@ int main(void) {
         return 6;
     }
     if (strlen(flc_last_error_string()) == 0) { printf("no error text\n"); return 7; }
+    /* TopK tie rule (flc_codec_params.tie): the zeroed struct selects FLC_TIE_LOWEST; both rules are
+     * accepted, anything else is rejected on the host before any device argument is looked at */
+    memset(&prm, 0, sizeof(prm));
+    prm.codec = FLC_TOPK;
+    prm.k = 10;
+    if (prm.tie != FLC_TIE_LOWEST || FLC_TIE_HIGHEST != 1) { printf("tie default\n"); return 11; }
+    prm.tie = 7;
+    if (flc_encode(&prm, NULL, NULL, 0, NULL, NULL, NULL, NULL, 0, NULL) != FLC_ERR_ARG ||
+        flc_encode_reduce(&prm, NULL, NULL, 0, NULL, 0, 0, NULL, 1.f, NULL, NULL, NULL, 0, NULL) != FLC_ERR_ARG ||
+        strstr(flc_last_error_string(), "tie") == NULL) {
+        printf("unknown tie rule must be rejected\n");
+        return 12;
+    }
+    prm.tie = FLC_TIE_HIGHEST;   /* accepted: d = 0 / n = 0 calls succeed without a device */
+    if (flc_encode_reduce(&prm, NULL, NULL, 0, NULL, 0, 0, NULL, 1.f, NULL, NULL, NULL, 0, NULL) != FLC_OK) {
+        printf("highest-index tie rule rejected\n");
+        return 13;
+    }
     /* the device-RNG host mirror */
     int64_t idx[10];
     if (flc_device_randk_indices(42, 3, 1000, 10, idx) != 0) { printf("randk indices\n"); return 8; }

@@ -1,0 +1,159 @@
+"""TopK tie rule in the ABI: flc_codec_params.tie chooses which of the
+entries tied at the K-th magnitude are kept when fewer places are left than ties — FLC_TIE_LOWEST
+(default; torch.topk's CPU order on the reference's rows, compressors.py:332) or FLC_TIE_HIGHEST.
+Every selection path of select.hip is driven with tied rows under the highest-index rule and checked
+bit-exactly against the oracle's topk_indices(tie="highest"), and shown to differ from the lowest-index
+result: the many-row fast path's tie cut (k_cand_select / k_cand_select_x), its exact fallback
+(exact_row, 512- and 1024-thread workgroups), the few-row spread select (k_cs_pass, list and
+histogram modes), the lone compressVector row (k_assign_finish), the dense-K path (k_radix_select
+FULLROW + k_topk_filter<EXACT>), both entry points and weights."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import codecs as oc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ag():
+    from flpytorch_amd import aggregation
+    return aggregation
+
+
+def _straddle(rows, k, g, places=(1, 3, 6), nties=(6, 9, 12)):
+    """Make row i's K-th magnitude tied by extra entries (mixed signs, spread over the row) with only
+    places[i % 3] places left at the cut."""
+    n, d = rows.shape
+    for i in range(n):
+        top, nt = places[i % 3] - 1, nties[i % 3]
+        mags = np.sort(np.abs(rows[i]))[::-1]
+        v = mags[k - 1 - top]
+        below = np.flatnonzero(np.abs(rows[i]) < mags[k + 10])
+        pos = below[np.linspace(0, len(below) - 1, nt).astype(np.int64)]
+        rows[i, pos] = v * np.where(g.random(nt) < 0.5, -1.0, 1.0).astype(np.float32)
+    return rows
+
+
+def _enc(rows, k, tie):
+    out = []
+    for r in rows:
+        e = np.zeros(r.size, dtype=np.float32)
+        ind = oc.topk_indices_fast(r, k, tie)
+        e[ind] = r[ind]
+        out.append(e)
+    return out
+
+
+def _bits(a):
+    return np.asarray(a.cpu().numpy() if torch.is_tensor(a) else a, dtype=np.float32).view(np.uint32)
+
+
+def _comp(ag, spec, d, tie, **kw):
+    c = ag.initCompressor(spec, d)
+    c.tie_policy = tie
+    for a, v in kw.items():
+        setattr(c, a, v)
+    return c
+
+
+@pytest.mark.parametrize("n,d,groups", [(256, 300_007, None), (256, 300_007, 2), (3, 2_000_000, None), (5, 10_000_000, None)])
+def test_fused_uplink_tie_rules(ag, n, d, groups):
+    """Fused encode+reduce of rows whose K-th magnitude is tied across the cut: the fast path's tie
+    cut (many rows: per-row-group selects; few rows: k_cs_pass) under both rules."""
+    k = math.ceil(0.01 * d)
+    g = np.random.default_rng([n, d, 3])
+    rows = _straddle(g.standard_normal((n, d)).astype(np.float32), k, g)
+    w = [float(v) for v in g.uniform(0.5, 2.0, n)]
+    rt = torch.from_numpy(rows).cuda()
+    got = {}
+    for tie in ("lowest", "highest"):
+        comp = _comp(ag, "topk:1%", d, tie, row_groups=groups)
+        assert comp.K == k
+        red = ag.UplinkReducer(comp)
+        enc = _enc(rows, k, tie)
+        got[tie] = red(rt)
+        np.testing.assert_array_equal(_bits(got[tie]), _bits(oc.reduce_plain(enc)))
+        np.testing.assert_array_equal(_bits(red([rt[i] for i in range(n)], weights=w)), _bits(oc.reduce_plain(enc, w)))
+        fl = ag.select_row_flags(red.comp, n, d).tolist()
+        assert all(f & 4 for f in fl), f"{tie}: expected the fast path's tie cut on every row, flags {sorted(set(fl))}"
+    assert not np.array_equal(_bits(got["lowest"]), _bits(got["highest"]))
+
+
+@pytest.mark.parametrize("kind", ["ties", "fewnz"])
+def test_fused_exact_fallback_tie_rules(ag, kind):
+    """Rows with more ties at the K-th key than the fast path gathers (or fewer than K nonzeros):
+    the exact fallback (exact_row) in the side selects of 128-row groups (512 threads) and in the last
+    group (1024 threads) keeps the tie rule."""
+    n, d = 256, 300_007
+    k = math.ceil(0.01 * d)
+    g = np.random.default_rng([len(kind), 9])
+    if kind == "ties":
+        rows = (g.integers(-3, 4, (n, d)) * 0.5).astype(np.float32)
+    else:
+        rows = np.zeros((n, d), dtype=np.float32)
+        rows[:, ::97] = g.standard_normal((n, len(range(0, d, 97)))).astype(np.float32)
+        rows[:, ::3 * 97] = 0.0
+    rt = torch.from_numpy(rows).cuda()
+    got = {}
+    for tie in ("lowest", "highest"):
+        red = ag.UplinkReducer(_comp(ag, "topk:1%", d, tie, row_groups=2))
+        got[tie] = red(rt)
+        np.testing.assert_array_equal(_bits(got[tie]), _bits(oc.reduce_plain(_enc(rows, k, tie))))
+        fl = np.asarray(ag.select_row_flags(red.comp, n, d))
+        assert np.all(fl & 8), "expected the exact path on every row"
+    if kind == "ties":                   # (fewnz: the tied K-th magnitude is 0, both rules add +0)
+        assert not np.array_equal(_bits(got["lowest"]), _bits(got["highest"]))
+
+
+@pytest.mark.parametrize("d,k,ties", [(2_000_003, 20_000, 40), (10_000_000, 100_000, 600), (4_000_000, 40_000, 3000)])
+def test_compressvector_tie_rules(ag, d, k, ties):
+    """A lone compressVector row (the drop-in): the spread select's tie cut (k_cs_pass) up to TIECAP
+    ties, the exact path (k_assign_finish's exact_row) beyond it."""
+    g = np.random.default_rng([d, ties])
+    x = g.standard_normal(d).astype(np.float32)
+    mags = np.sort(np.abs(x))[::-1]
+    v = mags[k - 1 - 7]
+    below = np.flatnonzero(np.abs(x) < mags[k + 10])
+    pos = below[np.linspace(0, len(below) - 1, ties).astype(np.int64)]
+    x[pos] = v * np.where(g.random(ties) < 0.5, -1.0, 1.0).astype(np.float32)
+    xt = torch.from_numpy(x).cuda()
+    outs = {}
+    for tie in ("lowest", "highest"):
+        c = _comp(ag, f"topk:{k}", d, tie)
+        outs[tie] = c.compressVector(xt)
+        want = _enc([x], k, tie)[0]
+        np.testing.assert_array_equal(_bits(outs[tie]), _bits(want))
+        f = int(ag.select_row_flags(c, 1, d)[0])
+        assert (f & 8) if ties > 2048 else (f & 4 and not f & 8), f"{tie}: flags {f}"
+    assert not np.array_equal(_bits(outs["lowest"]), _bits(outs["highest"]))
+
+
+def test_dense_k_tie_rules(ag):
+    """K > D / 16 (the multi-launch exact path: k_radix_select FULLROW, k_tie_count / k_tie_scan,
+    k_topk_filter<EXACT>) on tied rows, fused (both entry points) and compressVector."""
+    n, d = 4, 100_003
+    k = d // 5
+    g = np.random.default_rng(17)
+    rows = (g.integers(-6, 7, (n, d)) * 0.25).astype(np.float32)
+    rt = torch.from_numpy(rows).cuda()
+    got = {}
+    for tie in ("lowest", "highest"):
+        enc = _enc(rows, k, tie)
+        red = ag.UplinkReducer(_comp(ag, f"topk:{k}", d, tie))
+        got[tie] = red(rt)
+        np.testing.assert_array_equal(_bits(got[tie]), _bits(oc.reduce_plain(enc)))
+        np.testing.assert_array_equal(_bits(red([rt[i] for i in range(n)])), _bits(oc.reduce_plain(enc)))
+        c = _comp(ag, f"topk:{k}", d, tie)
+        np.testing.assert_array_equal(_bits(c.compressVector(rt[1])), _bits(enc[1]))
+    assert not np.array_equal(_bits(got["lowest"]), _bits(got["highest"]))
+
+
+def test_tie_rule_validation(ag):
+    c = ag.initCompressor("topk:1%", 1000)
+    c.tie_policy = "middle"
+    with pytest.raises(ValueError):
+        c.codec_params(torch.device("cuda"))
