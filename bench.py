@@ -503,6 +503,58 @@ def dropin(args):
                               "and uploads it; the second line reuses the drawn patterns"}))
 
 
+def dist_info(dist, dev, d, reps=5):
+    """What the process group really was, so that "RCCL saw N ranks" can be
+    checked from the bench line itself: the group's own world size and backend, every rank's host,
+    device index and PCI bus id (all_gather_object), the RCCL version torch links, and the time of
+    the step's exchange alone — an all-reduce of the [D] fp32 partial, timed after the bench's
+    timed region (max over ranks), with its ring bus bandwidth 2 (G-1)/G x bytes / t.  Collective:
+    every rank calls it.  Works on the gloo backend with CPU tensors (tests/test_bench_launcher.py)."""
+    import socket
+    import torch
+    g = dist.get_world_size()
+    backend = dist.get_backend()
+    me = {"rank": dist.get_rank(), "host": socket.gethostname(), "device": None, "pci_bus_id": None}
+    if dev.type == "cuda":
+        me["device"] = torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(dev)
+        bus = getattr(props, "pci_bus_id", None)
+        me["pci_bus_id"] = (f"{getattr(props, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(props, 'pci_device_id', 0):02x}"
+                            if isinstance(bus, int) else bus)
+        me["device_name"] = props.name
+    ranks = [None] * g
+    dist.all_gather_object(ranks, me)
+    ver = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            ver = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception as e:  # noqa: BLE001 — reported, not fatal
+            ver = f"unavailable ({type(e).__name__})"
+    t = torch.zeros(d, dtype=torch.float32, device=dev)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    dist.all_reduce(t)                                   # warm (communicator set up)
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(t)
+    sync()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    m = torch.tensor([ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    ms = float(m.item())
+    nbytes = 4 * d
+    return {"pg_world_size": g, "backend": backend, "rccl_version": ver, "ranks": ranks,
+            "distinct_devices": len({(r["host"], r["pci_bus_id"], r["device"]) for r in ranks}),
+            "allreduce_bytes": nbytes, "allreduce_ms": round(ms, 4),
+            "allreduce_busbw_GBps": round(2.0 * (g - 1) / g * nbytes / (ms * 1e-3) / 1e9, 3) if ms > 0 else None}
+
+
 def launch_ranks(gpus, cmd, poll_s=0.2, grace_s=10.0):
     """One process per GPU without an outside launcher (`python3 bench.py --gpus G`): G fresh
     children of ``cmd``, each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in its
@@ -781,6 +833,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ceiling = read_ceiling(rows, out)
+    mg = dist_info(dist, dev, d) if world > 1 else None
 
     step_ms = elapsed / args.steps * 1e3
     total_bytes = algorithmic_bytes(spec, n_total, d, k) if strong else algorithmic_bytes(spec, n, d, k, specs) * world
@@ -794,6 +847,8 @@ def main():
     kavg_ms = kms / max(klaunch, 1)
     kstep_ms = kms / args.steps
     achieved = kb / (kstep_ms * 1e-3) / 1e9 if klaunch else None
+    launches_per_step = klaunch / args.steps if klaunch else 0
+    kb_launch = kb / launches_per_step if launches_per_step else None
     line_floor = None
     if wl["kernel"] in ("k_randk_fold", "k_randk_gen"):
         # sparse 4-B gathers fetch whole 128-B lines (profiles/archive/r02/probe_gather_fetch.txt): the
@@ -865,7 +920,13 @@ def main():
             if (spec.startswith("randk") or mixed) else None,
             "roofline": {"bound": "hbm", "kernel": wl["kernel"],
                          "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+                         "frac": round(achieved / PEAK_GBS, 4) if achieved else None,
+                         # traffic: PMC HBM bytes of ONE launch (the contract's unit, like avg_launch_ms);
+                         # beside it the algorithmic bytes of one launch and their ratio, then the step's
+                         "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
+                         "algorithmic_bytes_per_launch": int(kb_launch) if kb_launch else None,
+                         "traffic_over_algorithmic": round(traffic / kb_launch, 4) if (traffic and kb_launch) else None,
+                         "traffic_per_step": int(traffic * launches_per_step) if (traffic and klaunch) else None,
                          "bytes_per_step": kb, "kernel_ms_per_step": round(kstep_ms, 4),
                          "kernel_timing": "HIP events around every launch on its stream, in a second pass of the "
                                           "same K steps after the timed region (the events would lengthen the step)",
@@ -882,6 +943,8 @@ def main():
         }
         if randk_group:
             line["randk_group"] = randk_group
+        if mg:
+            line["multi_gpu"] = mg
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -59,3 +59,21 @@ def test_bench_without_gpu_fails_loudly_not_hangs():
     if p.returncode == 0:
         pytest.skip("a GPU is visible here")
     assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def test_dist_info_fields_over_gloo(tmp_path):
+    """bench.dist_info (the multi_gpu block of a G > 1 bench line) on two gloo
+    ranks with CPU tensors: the group's world size and backend, one entry per rank, the exchange's
+    bytes and timing — the same function the GPU line calls over RCCL."""
+    out = tmp_path / "info.json"
+    code = ("import json, sys, torch, torch.distributed as dist; sys.path.insert(0, r'%s'); import bench;"
+            "dist.init_process_group('gloo');"
+            "i = bench.dist_info(dist, torch.device('cpu'), 1000, reps=2);"
+            "(open(r'%s', 'w').write(json.dumps(i)) if dist.get_rank() == 0 else None);"
+            "dist.destroy_process_group()") % (ROOT, out)
+    assert bench.launch_ranks(2, [sys.executable, "-c", code]) == 0
+    info = json.loads(out.read_text())
+    assert info["pg_world_size"] == 2 and info["backend"] == "gloo" and info["rccl_version"] is None
+    assert [r["rank"] for r in info["ranks"]] == [0, 1]
+    assert info["allreduce_bytes"] == 4000 and info["allreduce_ms"] > 0 and info["allreduce_busbw_GBps"] > 0
+    assert info["distinct_devices"] == 1          # CPU tensors: no device to tell the ranks apart

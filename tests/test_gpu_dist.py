@@ -131,6 +131,11 @@ def test_bench_self_launch_two_ranks():
                    "--no-cpu-baseline"])
     assert line["n_gpus"] == 2 and line["config"]["clients_total"] == 128
     assert line["scaling"] == "weak" and line["value"] > 0
+    # the multi_gpu block: what the process group really was
+    mg = line["multi_gpu"]
+    assert mg["pg_world_size"] == 2 and mg["backend"] == "gloo" and [r["rank"] for r in mg["ranks"]] == [0, 1]
+    assert all(r["device"] == 0 for r in mg["ranks"])          # the rehearsal shares cuda:0
+    assert mg["allreduce_bytes"] == 4 * 1_000_000 and mg["allreduce_ms"] > 0
 
 
 @pytest.mark.timeout(300)
