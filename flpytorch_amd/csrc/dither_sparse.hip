@@ -1171,11 +1171,40 @@ __device__ inline DsMeta ds_meta(const DsWs& ws, int64_t c, int64_t n, int64_t r
     return m;
 }
 
+// ds_meta without anything computed from the loads: off = sure entries, cnt = resolved entries
+// (their sum is the list length of a non-dense row), mode = the row's flags
+__device__ inline DsMeta ds_meta_raw(const DsWs& ws, int64_t c, int64_t n, int64_t rend, int64_t r, const float* w) {
+    DsMeta m;
+    m.off = 0; m.cnt = 0;
+    m.pn = 1.f; m.rpn = 1.f; m.w = 1.f; m.rk = 0; m.mode = 0;
+    if (r < rend) {
+        m.pn = ws.pn[r];
+        m.rpn = ws.rpn[r];
+        m.rk = ws.rk[r];
+        m.mode = ws.flags[r];
+        m.off = ws.tabs[c * n + r].y;
+        m.cnt = ws.cntr[c * n + r];
+        if (w) m.w = w[r];
+    }
+    return m;
+}
+
 #ifndef FLC_DS_MASKLD
 #define FLC_DS_MASKLD 0
 #endif
+#ifndef FLC_DS_L1REG
+#define FLC_DS_L1REG 0               // k_ds_accum (FLC_DS_WIDE): level-1 value from a register
+#endif
+#ifndef FLC_DS_LDSADD
+#define FLC_DS_LDSADD 0              // k_ds_accum (FLC_DS_WIDE): tile updates as LDS fp32 adds
+#endif
+#ifndef FLC_DS_WIDE
+#define FLC_DS_WIDE 1                // k_ds_accum (with FLC_DS_RAWRING): 64-row batches of list windows by LDS DMA
+                                     // (round 5: the fold 0.93 -> 0.70-0.73 ms per C4 step, step -0.05 ms, same
+                                     // allocation, profiles/r05/ab_c4_fold.txt)
+#endif
 #ifndef FLC_DS_RAWRING
-#define FLC_DS_RAWRING 0             // k_ds_accum: raw list loads in the ring, masked where folded
+#define FLC_DS_RAWRING 1             // k_ds_accum: raw list loads, masked where folded (the fast loop below)
 #endif
 #ifndef FLC_DS_AW
 #define FLC_DS_AW 1                  // waves per fold workgroup (LDS: one 8 KB tile per wave)
@@ -1184,7 +1213,11 @@ constexpr int DS_AW = FLC_DS_AW;
 #ifndef FLC_DS_AWPE
 #define FLC_DS_AWPE 0                // k_ds_accum: minimum waves per SIMD the register allocation targets (0: compiler's choice)
 #endif
-#if FLC_DS_AWPE > 0
+#if FLC_DS_WIDE
+// the compiler's occupancy model of the 16 KB of LDS per wave gives up on any waves-per-EU target
+// (it then takes 400 registers): cap the registers explicitly (4 waves per SIMD: 128)
+#define FLC_DS_ACCUM_ATTR __attribute__((amdgpu_num_vgpr(128)))
+#elif FLC_DS_AWPE > 0
 #define FLC_DS_ACCUM_ATTR __attribute__((amdgpu_waves_per_eu(FLC_DS_AWPE)))
 #else
 #define FLC_DS_ACCUM_ATTR
@@ -1205,6 +1238,7 @@ __global__ __launch_bounds__(64 * DS_AW) FLC_DS_ACCUM_ATTR void k_ds_accum(RowSr
     static_assert(64 % AP == 0, "row groups tile the 64-row batch");
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     __shared__ __attribute__((aligned(16))) float tile[DS_AW][HCHUNK];
+    __shared__ __attribute__((aligned(16))) uint16_t dstg[DS_AW][FLC_DS_WIDE ? 8 : 1][FLC_DS_WIDE ? 512 : 1];   // FLC_DS_WIDE: 8 KB per wave
     __shared__ float lvl[DS_MAXLEV + 1];
     if (threadIdx.x <= (unsigned)DS_MAXLEV) lvl[threadIdx.x] = (int)threadIdx.x <= s ? levels[threadIdx.x] : 0.f;
     __syncthreads();
@@ -1281,10 +1315,101 @@ __global__ __launch_bounds__(64 * DS_AW) FLC_DS_ACCUM_ATTR void k_ds_accum(RowSr
         // and its use: each row waits for its own load only (a static vmcnt(AP - 1)).  (The
         // previous form masked at the load and took a general path inside the same loop: the
         // compiler copied the ring at the back-edges and waited for the whole ring there.)
+        int64_t b = 0;
+#if FLC_DS_WIDE
+        cur = ds_meta_raw(ws, h, n, rend, r0 + lane, w);
+        const float lv1 = lvl[1];
+        // Wide batches through LDS DMA: a 64-row batch's list windows (the first 128 B of each row's
+        // region) are 8 loads of 16 B per lane straight into the wave's 8 KB staging (lane l: row
+        // l / 8 of its 8-row slot, bytes 16 (l % 8) ..; no ring registers), issued a whole batch
+        // ahead.  The compiler waits for every outstanding load before the first staging read
+        // (vmcnt(0): it does not track LDS DMA per slot), so each batch reads all its 64 entries
+        // per lane first, then issues the next batch's 8 loads and its row state, then folds the
+        // 64 rows: each batch's loads have a whole batch of folding to arrive in (the 16-row
+        // register ring waited a memory latency every 16 rows).
+        auto dma = [&](int64_t row0, int sl) {
+            const uint16_t* src = ws.ent16 + (h * n + min(row0 + (lane >> 3), n - 1)) * DS_HCAP + (lane & 7) * 8;
+            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&dstg[wv][sl][0], 16, 0, 0);
+        };
+#pragma unroll
+        for (int sl = 0; sl < 8; ++sl) dma(r0 + 8 * sl, sl);
+        for (; b < nb; ++b) {
+            const int64_t i0 = r0 + b * 64;
+            if (__ballot((cur.mode & DS_DENSE) != 0u) != 0ull) break;
+            // rows with more than 64 entries in this half (~1e-4 of C4's): the batch takes the rolled
+            // path below, which reads the rest of their lists directly
+            const uint64_t lng = __ballot(cur.off + cur.cnt > 64u);
+            if (__builtin_expect(lng == 0ull, 1)) {
+                // the batch's 64 entries of this lane, two rows per register
+                uint32_t ent2[32];
+#pragma unroll
+                for (int q = 0; q < 64; q += 2)
+                    ent2[q >> 1] = (uint32_t)dstg[wv][q >> 3][(q & 7) * 64 + lane] |
+                                   ((uint32_t)dstg[wv][(q + 1) >> 3][((q + 1) & 7) * 64 + lane] << 16);
+                __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): the slots are read
+                // the next batch's row state, raw (nothing computed from it before the next batch: a
+                // use here would wait for the loads behind it), then its list windows
+                nxt = ds_meta_raw(ws, h, n, rend, i0 + 64 + lane, w);
+#pragma unroll
+                for (int sl = 0; sl < 8; ++sl) dma(i0 + 64 + 8 * sl, sl);
+#pragma unroll
+                for (int q = 0; q < 64; ++q) {
+                    // rows in order; the scheduler does not hoist 64 rows' work (register pressure)
+                    __builtin_amdgcn_sched_barrier(0);
+                    float pn, wi;
+                    row_state(cur, q, pn, wi);
+                    // (no dense row in the batch: the count is the sure + resolved entries)
+                    const uint32_t cnt = __builtin_amdgcn_readlane(cur.off, q) + __builtin_amdgcn_readlane(cur.cnt, q);
+                    const uint32_t raw = (q & 1) ? (ent2[q >> 1] >> 16) : (ent2[q >> 1] & 0xFFFFu);
+                    const uint32_t a = (uint32_t)lane < cnt ? raw : NONE;
+#if FLC_DS_L1REG
+                    // level 1 (every sure entry, most resolved ones) from a register: the row's chain
+                    // keeps one LDS round trip (the tile's) instead of two
+                    float lv = lv1;
+                    if (__builtin_expect(__ballot(a != NONE && ((a >> 12) & 15u) != 1u) != 0ull, 0)) lv = lvl[(a >> 12) & 15u];
+                    const float e = __uint_as_float(__float_as_uint(lv) | ((a & 0x800u) << 20)) * pn;
+#else
+                    const float e = value(a, pn);
+#endif
+                    if (a != NONE) {
+                        const float t = W ? wi * e : e;
+#if FLC_DS_LDSADD
+                        // LDS fp32 add without return: one wave's LDS operations run in issue order, so
+                        // each column still takes its rows' terms in row order; no read in the chain
+                        if (!(t == 0.f)) atomicAdd(&tl[a & (HCHUNK - 1)], t);
+#else
+                        add(a & (HCHUNK - 1), t);
+#endif
+                    }
+                }
+            } else {
+#pragma unroll 1
+                for (int q = 0; q < 64; ++q) {
+                    float pn, wi;
+                    row_state(cur, q, pn, wi);
+                    const uint32_t cnt = __builtin_amdgcn_readlane(cur.off, q) + __builtin_amdgcn_readlane(cur.cnt, q);
+                    const uint32_t raw = dstg[wv][q >> 3][(q & 7) * 64 + lane];
+                    const uint32_t a = (uint32_t)lane < cnt ? raw : NONE;
+                    const float e = value(a, pn);
+                    if (a != NONE) add(a & (HCHUNK - 1), W ? wi * e : e);
+                    const int64_t row = i0 + q;
+                    for (uint32_t kk = 64u + lane; kk < cnt; kk += 64) {
+                        const uint32_t en = ws.ent16[(h * n + row) * DS_HCAP + kk];
+                        const float ev = value(en, pn);
+                        add(en & (HCHUNK - 1), W ? wi * ev : ev);
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): the slots are read
+                nxt = ds_meta_raw(ws, h, n, rend, i0 + 64 + lane, w);
+#pragma unroll
+                for (int sl = 0; sl < 8; ++sl) dma(i0 + 64 + 8 * sl, sl);
+            }
+            cur = nxt;
+        }
+#else
         const uint16_t* hb = ws.ent16 + h * n * DS_HCAP + lane;
 #pragma unroll
         for (int q = 0; q < AP; ++q) ra[q] = hb[min(r0 + q, n - 1) * DS_HCAP];
-        int64_t b = 0;
         // 64-row batches (the last one may be partial: its rows past the end have count 0) until
         // one holds a dense row; from there the rows go one at a time below
         for (; b < nb; ++b) {
@@ -1315,6 +1440,7 @@ __global__ __launch_bounds__(64 * DS_AW) FLC_DS_ACCUM_ATTR void k_ds_accum(RowSr
             }
             cur = nxt;
         }
+#endif
         // rows from the batch with a dense row on, one at a time (rare: a row outside its sample's
         // norm bounds, an overflowed item, a non-finite row or weight)
         for (int64_t row = r0 + b * 64; row < rend; ++row) {
@@ -1484,6 +1610,9 @@ static_assert(FLC_DS_LASTPCT >= 1 && FLC_DS_LASTPCT <= 100, "FLC_DS_LASTPCT: the
 #ifndef FLC_DS_SIDE_RES_WG
 #define FLC_DS_SIDE_RES_WG 0         // a non-last row group's resolve: grid cap, 0 = one wave per 64 items
 #endif
+#ifndef FLC_DS_PROBE_SIDE
+#define FLC_DS_PROBE_SIDE 0          // A/B probes: 1 skip the side resolve, 2 the side fold, 3 both (outputs NOT valid)
+#endif
 #ifndef FLC_DS_PROBE_DEF
 #define FLC_DS_PROBE_DEF 0           // A/B variant builds only (a probe's outputs are NOT valid)
 #endif
@@ -1637,6 +1766,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         // beside the next group's filter: a bounded grid (grid-stride), so the side kernel holds a
         // fixed share of the CUs instead of taking every slot a retiring filter block frees
         if (beside && FLC_DS_SIDE_RES_WG > 0) rb = std::min(rb, FLC_DS_SIDE_RES_WG);
+        if (!(beside && (FLC_DS_PROBE_SIDE & 1)))             // probe builds only (outputs NOT valid)
         { ProfScope _ps("k_ds_resolve", sr);
         hipLaunchKernelGGL(compat ? k_ds_resolve<true> : k_ds_resolve<false>, dim3(rb), dim3(256), 0, sr, n, r0, rn, ws,
                            prm->d_levels, prm->s, us); }
@@ -1712,7 +1842,8 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
             }
         }
         if (rc) return rc;
-        rc = accum(r0, r1 - r0, g == 0, g == K - 1, cx.side, g < K - 1);
+        if (!(g < K - 1 && (FLC_DS_PROBE_SIDE & 2)))         // probe builds only (outputs NOT valid)
+            rc = accum(r0, r1 - r0, g == 0, g == K - 1, cx.side, g < K - 1);
         if (rc) return rc;
     }
     FLC_CHECK_HIP(hipEventRecord(cx.ev[K], cx.side));
