@@ -34,7 +34,7 @@ def _device(device):
 def select_row_flags(comp: Compressor, n, d, device=None):
     """Path report of the last TopK call on the current stream's workspace (flc_select_row_flags): a
     [n] int64 tensor of row state bits — 1 overflow, 2 short list, 4 ties cut on the fast path,
-    8 exact path.  Call it right after the UplinkReducer / compressVector call, with its n and d
+    8 exact path, 16 a lone row selected in registers (compressVector, D <= 16.7 M).  Call it right after the UplinkReducer / compressVector call, with its n and d
     (compressVector: n = 1).  Tests use it to assert which path ran."""
     dev = _device(device)
     lib = _lib.load()

@@ -40,6 +40,7 @@ namespace flc {
 
 constexpr uint32_t ALL = 0xFFFFFFFFu;
 constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
+constexpr uint32_t F_RESIDENT = 16u;  // a lone row selected exactly in registers (k_lone_resident)
 constexpr int SMAX = 16384;          // sample size kept in LDS
 constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
 constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
@@ -47,8 +48,31 @@ constexpr int CS_SH = 64;            // few rows: shards of a row's candidate li
 constexpr int64_t CS_FEW = 16;       // rows: sharded lists + k_cs_pass up to here, else k_cand_select
 constexpr int CS_ST = 8;             // words of a row's k_cs_pass state
 constexpr int CS_LCAP = 2048;        // entries of the first digit's bin ranked directly (list mode)
+constexpr int RS_U = 16;             // (<= 16: kept-tie mask of 64 bits) k_lone_resident: float4 of the row per thread at most (64 VGPRs)
+#ifndef FLC_RS_NG
+#define FLC_RS_NG 4                   // k_lone_resident: workgroup groups (histogram replicas, barrier tree);
+#endif                                // us a call at D = 10 M: 1 -> 57, 2 -> 53, 4 -> 52, 8 -> 54.6, 16 -> 60
+constexpr int RS_NG = FLC_RS_NG;
+// its control words: counters on lines of their own, per-group digit histograms, tie counts
+constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128;
+constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
+constexpr int RS_HREP = RS_GRP + 32 * RS_NG;
+constexpr int RS_CLIST = RS_HREP + 3 * RS_NG * HBINS;    // [RS_CAP] (value bits, index)
+constexpr int RS_TCNT = RS_CLIST + 2 * RS_CAP;
+#ifdef FLC_RS_PRINT
+constexpr int RS_PROBE = RS_TCNT + 2048;   // probe builds: per-workgroup start / arrival stamps
+constexpr int RS_CTL = RS_PROBE + 4096;
+#else
+constexpr int RS_CTL = RS_TCNT + 2048;     // (tie counts: 64-bit (call << 32 | count) per workgroup)
+#endif
 #ifndef FLC_CS_LIST
 #define FLC_CS_LIST 1
+#endif
+#ifndef FLC_LONE_HSMAX
+#define FLC_LONE_HSMAX 1             // largest lone-row histogram stride (words) the workspace holds
+#endif
+#ifndef FLC_LONE_HS
+#define FLC_LONE_HS 1                 // its stride (1: contiguous; 32 / 64 / 1056 measured no different)
 #endif
 #ifndef FLC_CS_TWO_MAXD
 #define FLC_CS_TWO_MAXD (int64_t(64) << 20)   // rows up to this long: two k_cs_pass launches
@@ -78,6 +102,8 @@ struct SelWs {            // carved from the caller workspace
     float* part;          // [D] TopK row-group folds: the running tiles carried from one group to the next
     int64_t cap;
     uint32_t tie_hi;      // TopK ties at the K-th key: 0 the lowest indices are kept (default), 1 the highest
+    uint32_t* lhist;      // [HBINS * FLC_LONE_HSMAX] a lone row's first-digit histogram (k_lone_finish path), bin b
+    uint32_t lh_stride;   // at word b * lh_stride (spread over memory channels: its atomics come from every CU)
 };
 
 // Tie order of TopK (flc_codec_params.tie): tie_pref(ix) is larger for the index kept first among
@@ -168,13 +194,30 @@ __device__ inline uint32_t key_bin(uint32_t key, int p) {
 // ------------------------------------------------------------------------------------------
 // DUAL (few rows: latency-bound): the two rank searches share their passes over the sample; the
 // second histogram costs 8 KB of LDS, which would halve the workgroups per CU of a many-row launch.
+// zout (a lone compressVector row, k_lone_finish path): the workgroups past the n sample ones write
+// the dense output's zeros, one wave per 4096-element chunk (the chip is idle beside the one
+// latency-bound sample workgroup; the filter then only reads)
 template <int NT, bool DUAL>
-__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few) {
+__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few,
+                                                    int lone, float* __restrict__ zout) {
     __shared__ uint32_t keys[SMAX];
     __shared__ uint32_t h[HBINS], h2[DUAL ? HBINS : 1];
     __shared__ uint32_t scratch[260], scratch2[DUAL ? 260 : 1];
     const int64_t row = blockIdx.x;
-    if (row >= n) return;
+    if (row >= n) {
+        if (!zout) return;
+        constexpr int WPB = NT / 64;
+        const int lane = threadIdx.x & 63;
+        const int64_t C = nchunks(d), wstride = (int64_t)(gridDim.x - n) * WPB;
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        const u4v z = {0u, 0u, 0u, 0u};
+        for (int64_t c = (row - n) * WPB + (threadIdx.x >> 6); c < C; c += wstride) {
+            const auto ro = chunk_rsrc(zout, c * CHUNK, d);                 // range-checked: the last chunk
+#pragma unroll
+            for (int L = 0; L < 16; ++L) __builtin_amdgcn_raw_buffer_store_b128(z, ro, lane * 16, L * 1024, 0);
+        }
+        return;
+    }
     const float* r = rows.row(row);
     // sample: the whole row if it fits, else P pieces of 256 contiguous elements spread evenly
     int S;
@@ -272,6 +315,8 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
     if (few && threadIdx.x < CS_SH) ws.shcnt[(row * CS_SH + threadIdx.x) * RCS] = 0;
     if (few)                                              // the row's global histogram of k_cs_pass
         for (int i = threadIdx.x; i < HBINS; i += NT) ws.hist[row * HBINS + i] = 0;
+    if (lone)                                             // the lone row's (k_lone_finish path)
+        for (int i = threadIdx.x; i < HBINS; i += NT) ws.lhist[(size_t)i * ws.lh_stride] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -795,7 +840,7 @@ static_assert(GCAP % 64 == 0, "copy-out runs in whole wave slots");
 // loads deep (the next chunk's descriptor is built up front; past the last item it has
 // num_records 0 and its loads return zeros without touching memory).
 // FGS: chunks per work item (group).
-template <int RING, int FGS, bool ZF = false>
+template <int RING, int FGS, int LONE = 0>
 #ifndef FLC_TK_RING
 #define FLC_TK_RING 16               // loads in flight per wave (ring registers: 4 x RING VGPRs)
 #endif
@@ -808,8 +853,11 @@ template <int RING, int FGS, bool ZF = false>
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
-// ZF (a lone compressVector row): every float4 read is also written as zeros to zout, the dense
-// output the selected entries are then scattered into (no separate fill of the output).
+// LONE (a lone compressVector row): 1 — every float4 read is also written as zeros to zout, the
+// dense output the selected entries are then scattered into (no separate fill of the output);
+// 2 — the k_lone_finish path: the zeros are written beside the sample, and every staged entry adds
+// one to the row's first-digit histogram (k_cs_pass's first digit, memory-side atomics at the
+// group's copy-out), so the one launch after the filter can pick the digit itself.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, SelWs ws, int shards,
                                                                                                 float* __restrict__ zout) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
@@ -918,6 +966,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
             }
         }
 #endif
+        if constexpr ((LONE & 2) != 0) {
+            // first digit of dk = key - T over the row's histogram (k_cs_pass's, same shift)
+            if (fits && ptot) {
+                const uint32_t Tr = sload(ws.thr + prow), span = sload(ws.prefix + prow) - Tr;
+                uint32_t s0 = 0;
+                while (s0 < 21 && (((uint64_t)span * 4u) >> s0) >= (uint64_t)HBINS) ++s0;
+                uint32_t* gh = ws.lhist;                                 // lone row: prow == 0
+                const uint32_t hs = ws.lh_stride;
+                const float* svf = reinterpret_cast<const float*>(st[pb][wv] + SROW);
+                // not the clamp bin (HBINS - 1: every key past the first digit's range, the row's largest
+                // — ~10-20 K entries on one address, whose atomics serialise: 0.35 ms a call measured);
+                // k_lone_finish takes its count as the list's total minus the other bins
+                for (uint32_t e = (uint32_t)lane; e < ptot; e += 64) {
+                    const uint32_t dg = (mag_key(svf[e]) - Tr) >> s0;
+                    if (dg < (uint32_t)(HBINS - 1))
+                        __hip_atomic_fetch_add(gh + (size_t)dg * hs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
     };
     while (it < items) {
         // key >= max(T, 1): the loads past the row end return +0 (key 0), so no per-element range
@@ -949,7 +1016,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
             }
             const uint32_t cnt0 = cnt;
             __amdgpu_buffer_rsrc_t ro;
-            if constexpr (ZF) ro = chunk_rsrc(zout, j0, d);
+            if constexpr ((LONE & 1) != 0) ro = chunk_rsrc(zout, j0, d);
             // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
             // component) index constants out of the loop into 64 live VGPRs
             uint32_t lb = (uint32_t)j0 + (uint32_t)lane * 4u;   // row index of the lane's element 0
@@ -959,7 +1026,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 const int P = L + RING - 1;
                 ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
                 const float4 x = ring[L % RING];
-                if constexpr (ZF) {
+                if constexpr ((LONE & 1) != 0) {
                     // unconditional (range-checked): one more store per step in the vmcnt queue
                     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
                     const u4v z = {0u, 0u, 0u, 0u};
@@ -2294,6 +2361,564 @@ __global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d,
     }
 }
 
+// A lone compressVector row, the short path: after k_topk_sample wrote the output's zeros and
+// k_topk_filter_fast<LONE = 2> left the row's first-digit histogram, the digit, the ranking of its bin
+// and the scatter in ONE launch (instead of k_cs_pass x 2 + k_assign_finish).  Every workgroup reads
+// the histogram and picks the first digit itself (hist_find: k_cs_pass's first pass, same bin), then
+// walks its shard of the list: entries above the digit's bin are in the top K whatever the rest
+// (their keys exceed every key of the bin, which holds the K-th) and are scattered at once; entries
+// in the bin go to the row's bin list (k_cs_pass list mode).  The last workgroup to arrive ranks the
+// bin's entries by (key desc, tie order) — the K-th key and the tie cut at once — and scatters the
+// admitted ones.  A row the digit does not settle (overflow, short list, K-th key in the clamp bin,
+// a bin over CS_LCAP entries, a count mismatch) takes exact_row in one workgroup, which scatters its
+// rewritten list (any entry scattered before is in it, with the same value).  Row state as k_cs_pass
+// leaves it (thr, krem, tiecut, flags: flc_select_row_flags).
+template <bool VEC>
+__global__ __launch_bounds__(EX_NT) void k_lone_finish(RowSrc rows, int64_t d, int64_t K, SelWs ws, float* __restrict__ out) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t wsum[EX_NT / 64];
+    __shared__ uint64_t lst[CS_LCAP];
+    __shared__ uint64_t kth_s;
+    __shared__ uint32_t last_wg;
+    const uint32_t b = blockIdx.x, B = gridDim.x;                        // B == CS_SH: shard b
+    uint32_t cnt = 0;
+    for (int k = 0; k < CS_SH; ++k) cnt += ws.shcnt[k * RCS];
+    const uint32_t T = ws.thr[0], span = ws.prefix[0] - T;              // kest >= T
+    uint32_t s0 = 0;
+    while (s0 < 21 && (((uint64_t)span * 4u) >> s0) >= (uint64_t)HBINS) ++s0;
+    auto exact = [&]() {
+        if (threadIdx.x == 0 && ws.flags[0] == 0u) ws.flags[0] = F_SHORT;
+        exact_row<VEC>(rows, 1, 0, d, K, ws, h, scratch, wsum);
+        __threadfence_block();
+        const uint32_t c = ws.rowcnt[0];
+        for (uint32_t e = threadIdx.x; e < c; e += EX_NT) out[ws.ent_idx[e]] = ws.ent_val[e];
+    };
+    // read once per workgroup (workgroup 0 may set flags below while others read them): a workgroup
+    // seeing flags set by workgroup 0's exact path returns as it does, so the outcome is the same
+    if (threadIdx.x == 0) last_wg = (ws.flags[0] != 0u || cnt < (uint32_t)K) ? 1u : 0u;
+    __syncthreads();
+    bool fail = last_wg != 0u;
+    __syncthreads();
+    uint32_t bin = 0, above = 0, last = 0;
+    if (!fail) {
+        if (threadIdx.x == 0) scratch[259] = 0;
+        __syncthreads();
+        uint32_t part = 0;
+        for (int t = threadIdx.x; t < HBINS - 1; t += EX_NT) { const uint32_t v = ws.lhist[(size_t)t * ws.lh_stride]; h[t] = v; part += v; }
+        part = wave_sum(part);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&scratch[259], part);
+        __syncthreads();
+        if (threadIdx.x == 0) h[HBINS - 1] = cnt - scratch[259];          // the clamp bin: not counted by the filter
+        __syncthreads();
+        hist_find(h, (uint32_t)K, bin, above, scratch);
+        last = h[bin];
+        fail = bin == HBINS - 1 || last > (uint32_t)CS_LCAP;
+    }
+    if (fail) {
+        if (b == 0) exact();
+        return;
+    }
+    const uint32_t krem = (uint32_t)K - above;                           // >= 1: the K-th is in the bin
+    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
+    const uint32_t mycnt = ws.shcnt[b * RCS];
+    const float* sv = ws.ent_val + b * segcap;
+    const uint32_t* si = ws.ent_idx + b * segcap;
+    if (threadIdx.x == 0) scratch[0] = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < mycnt; e += EX_NT) {
+        const float v = sv[e];
+        const uint32_t ix = si[e], key = mag_key(v);
+        const uint32_t dg = min((key - T) >> s0, (uint32_t)(HBINS - 1));
+        if (dg > bin) {
+            out[ix] = v;
+        } else if (dg == bin) {
+            const uint32_t slot = atomicAdd(&scratch[0], 1u);
+            if (slot < (uint32_t)CS_LCAP) lst[slot] = ((uint64_t)key << 32) | (uint64_t)tie_pref(ix, ws.tie_hi);
+        }
+    }
+    __syncthreads();
+    const uint32_t nl = min(scratch[0], (uint32_t)CS_LCAP);
+    if (threadIdx.x == 0) scratch[1] = nl ? atomicAdd(&ws.cstate[5], nl) : 0u;
+    __syncthreads();
+    uint64_t* gl = ws.clist;
+    const uint32_t gb = scratch[1];
+    for (uint32_t i = threadIdx.x; i < nl; i += EX_NT)
+        if (gb + i < (uint32_t)CS_LCAP) gl[gb + i] = lst[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                     // list and scatter stores done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        last_wg = atomicAdd(&ws.carrive[0], 1u) == B - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last_wg) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (threadIdx.x == 0) atomicExch(&ws.carrive[0], 0u);
+    const uint32_t m = __hip_atomic_load(&ws.cstate[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(m == last && m >= krem)) {                                     // every entry of the bin arrived
+        exact();
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < m; i += EX_NT)
+        lst[i] = __hip_atomic_load(&gl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) { scratch[2] = 0; scratch[3] = 0; }
+    __syncthreads();
+    // the entry of rank krem - 1 is the K-th: its key the threshold, its index the tie cut
+    for (uint32_t i = threadIdx.x; i < m; i += EX_NT) {
+        const uint64_t me = lst[i];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < m; ++j) rank += lst[j] > me ? 1u : 0u;
+        if (rank == krem - 1u) kth_s = me;                               // entries are distinct
+    }
+    __syncthreads();
+    const uint64_t kc = kth_s;
+    const uint32_t kth = (uint32_t)(kc >> 32);
+    const float* r = rows.row(0);
+    for (uint32_t i = threadIdx.x; i < m; i += EX_NT) {
+        const uint64_t me = lst[i];
+        const uint32_t key = (uint32_t)(me >> 32);
+        if (me >= kc) {
+            const uint32_t ix = tie_pref((uint32_t)me, ws.tie_hi);      // tie_pref is its own inverse
+            out[ix] = r[ix];
+        }
+        if (key > kth) atomicAdd(&scratch[2], 1u);
+        else if (key == kth) atomicAdd(&scratch[3], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t gt = scratch[2], eq = scratch[3];
+        ws.thr[0] = kth;
+        ws.krem[0] = krem - gt;                                          // ties admitted
+        if (gt + eq > krem) { ws.tiecut[0] = tie_pref((uint32_t)kc, ws.tie_hi); ws.flags[0] |= F_TIES; }
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// A lone compressVector row held in the chip's registers: the exact selection in ONE launch.
+// The row (up to RS_U float4 a thread x 1024 threads x one workgroup per CU: 16.7 M elements on 256
+// CUs, 64 MB of the chip's 128 MB of VGPRs) is read once into registers; the exact radix select
+// (11/11/9-bit digits of the magnitude key, exact_row's digits) runs over it: per digit, each
+// workgroup's LDS histogram is added into its group's replica (RS_NG groups: the atomics on one
+// address come from G / RS_NG workgroups, not G — one global histogram's hot bins serialised 245
+// deep), the workgroups arrive through a two-level counter tree, and the last to arrive sums the
+// replicas, picks the digit (hist_find) and releases the others with the result in the release
+// word.  After two digits the elements sharing the K-th key's 22-bit prefix (~70 on a Gaussian
+// 10 M row, at most RS_CAP) are listed and ranked by the last workgroup to arrive (key, then tie
+// order), which stores the kept ones; everyone else has written its dense output (x where the
+// prefix is above, +0 elsewhere) and left.  Rows with more elements at that prefix take the third
+// digit and a tie-rank exchange (workgroups publish their tie counts, tagged by the call's sequence
+// number; one holding ties sums those before it).  No sample, no candidate lists, no fallback.
+// The grid must be co-resident: one 1024-thread workgroup per CU, G <= CUs, and the launches are
+// serialised across streams (select.hip host code); a wait past FLC_RS_SPIN ticks of the 100 MHz
+// clock gives up and flags the row (F_OVERFLOW) instead of hanging.  The control block is the
+// library's own, zeroed once; every call leaves it clean (self-resetting barrier counters, replicas
+// cleared by their merger).
+// ------------------------------------------------------------------------------------------
+constexpr int RS_NT = 1024;
+#ifndef FLC_RS_SPIN
+#define FLC_RS_SPIN 10000000ull          // 0.1 s of the 100 MHz clock
+#endif
+
+struct RsTree {
+    uint32_t* ctl;
+    uint32_t grp, gsz, ngr;             // this workgroup's group, its size, groups in use
+};
+// The release word (64 bits at RS_GEN): generation mod 16 | the digit's bin << 4 | the count above it
+// << 15 (24 bits: < K <= 2^24) | the bin's count << 39 (25 bits): the waiters get the merger's result
+// with the release itself.
+__device__ inline uint64_t rs_word(uint32_t gen, uint32_t bin, uint32_t above, uint32_t last) {
+    return (uint64_t)(gen & 15u) | ((uint64_t)bin << 4) | ((uint64_t)above << 15) | ((uint64_t)last << 39);
+}
+// Self-resetting two-level barrier (no per-call clearing): a group's counter is reset by its last
+// arriver, the global one by the last group's; every workgroup reads the release word BEFORE
+// arriving and waits for its generation to change (the merger bumps it after every arrival, so no
+// workgroup can have read the new one).  rs_arrive returns true on the last workgroup to arrive (the
+// merger), whose thread 0 has acquired every other workgroup's writes.
+// (gen: the release word's generation, read by thread 0 before this workgroup's flush — any time
+// after the previous release — so that its load is not one more round trip here)
+__device__ inline uint32_t rs_gen(const RsTree& tr) {
+    return (uint32_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 15u;
+}
+__device__ inline bool rs_arrive(const RsTree& tr, uint32_t* flag_s, uint32_t* gen_s, uint32_t gen) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                     // this wave's atomics performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *gen_s = gen;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        uint32_t last = 0;
+        uint32_t* gc = tr.ctl + RS_GRP + 32 * tr.grp;
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tr.gsz - 1u) {
+            __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (__hip_atomic_fetch_add(tr.ctl + RS_GLOB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tr.ngr - 1u) {
+                __hip_atomic_store(tr.ctl + RS_GLOB, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+        }
+        *flag_s = last;
+    }
+    __syncthreads();
+    return *flag_s != 0u;
+}
+// the merger, after its writes: the release word with its result
+__device__ inline void rs_release(const RsTree& tr, const uint32_t* gen_s, uint32_t bin, uint32_t above, uint32_t last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(tr.ctl + RS_GEN), rs_word(*gen_s + 1u, bin, above, last), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// everyone else: the release word (thread 0 leaves it in res_s[0..2] = bin, above, last)
+__device__ inline void rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t* res_s) {
+    if (threadIdx.x == 0) {
+        const uint64_t* rw = reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN);
+        const uint64_t t0 = (uint64_t)wall_clock64();
+        uint64_t w;
+        while (((uint32_t)(w = __hip_atomic_load(rw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 15u) == *gen_s) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((uint64_t)wall_clock64() - t0 > FLC_RS_SPIN) {
+                __hip_atomic_fetch_or(tr.ctl + RS_GAVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        res_s[0] = (uint32_t)(w >> 4) & 0x7FFu;
+        res_s[1] = (uint32_t)(w >> 15) & 0xFFFFFFu;
+        res_s[2] = (uint32_t)(w >> 39);
+    }
+    __syncthreads();
+}
+
+#ifdef FLC_RS_PRINT                       // probe builds: phase stamps of workgroup 0 (printf)
+#define RS_STAMP(i) do { if (threadIdx.x == 0) stamp[i] = (uint64_t)wall_clock64(); } while (0)
+#else
+#define RS_STAMP(i) do { } while (0)
+#endif
+template <int RU>
+__global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d, int64_t K, SelWs ws,
+                                                          float* __restrict__ out, int e4, uint32_t* __restrict__ ctl,
+                                                          uint32_t seq) {
+    __shared__ uint32_t h[HBINS];
+    __shared__ uint32_t scratch[260];
+    __shared__ uint32_t wsum[RS_NT / 64];
+    __shared__ uint32_t flag_s, gen_s;
+    const uint32_t G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+#ifdef FLC_RS_PRINT
+    uint64_t stamp[16] = {0};
+#endif
+    RS_STAMP(0);
+    RsTree tr;
+    tr.ctl = ctl;
+    tr.grp = g % RS_NG;
+    tr.ngr = min(G, (uint32_t)RS_NG);
+    tr.gsz = (G - tr.grp + RS_NG - 1) / RS_NG;
+    const uint32_t nb = (uint32_t)(d * 4);                               // d <= RS_U * 4096 * CUs
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(0)), (short)0, (int)nb, 0x00020000);
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)nb, 0x00020000);
+    // float4 u of this thread: elements 4 (g e4 RS_NT + u RS_NT + t) + q, coalesced over the threads;
+    // index order inside the workgroup is (u, t, q), workgroups in order (G = ceil(d / (4 e4 RS_NT))).
+    // A thread's float4 u < uv lie (at least partly) inside the row; the rest are skipped.  The one
+    // float4 that straddles the row end holds pad = (-d) mod 4 elements of +0 (the range-checked
+    // load): padding at the END of the index order, taken out of the counts of key 0 (bin 0 while
+    // the digits so far are 0; the tie count of the workgroup holding it when the K-th key is 0),
+    // never stored.  (Whole padding float4 counted into bin 0 serialised ~40 K LDS atomics on one
+    // address in the last workgroups: 40 us.)
+    const uint32_t f0 = g * (uint32_t)e4 * RS_NT + t;                   // float4 index of u = 0
+    const int64_t d4 = (d + 3) / 4;                                      // float4 touching the row
+    const int uv = (int)min((int64_t)e4, max((int64_t)0, (d4 - (int64_t)f0 + RS_NT - 1) / RS_NT));
+    const uint32_t pad = (uint32_t)((4 - (d & 3)) & 3);
+    const uint32_t padg = (uint32_t)((d / 4) / ((int64_t)e4 * RS_NT));  // the workgroup holding it
+    const uint32_t voff = f0 * 16u;
+    float4 v[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+        if (u < uv) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rx, voff, u * RS_NT * 16, FLC_LOADPOL);
+            v[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
+        }
+    }
+    uint32_t prefix = 0, krem = (uint32_t)K, last = 0, bar = 0;
+    bool cand = false;
+    for (int p = 0; p < 3; ++p) {
+        const uint32_t gen = t == 0 ? rs_gen(tr) : 0u;                   // (in flight under the histogram)
+        for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
+        __syncthreads();
+        // an opaque copy of the key mask per pass: keeps the compiler from hoisting the 4 RU keys out
+        // of the pass loop into as many more VGPRs (spills at 128)
+        uint32_t km = 0x7FFFFFFFu;
+        asm volatile("" : "+s"(km));
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            if (u < uv) {
+                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t k = __float_as_uint(e[q]) & km;
+                    if (key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
+                }
+            }
+        }
+        __syncthreads();
+        RS_STAMP(1 + 3 * p);
+#ifdef FLC_RS_PRINT
+        if (t == 0 && p == 0) {
+            uint64_t* pr = reinterpret_cast<uint64_t*>(ctl + RS_PROBE);
+            __hip_atomic_store(pr + g, stamp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(pr + 1024 + g, stamp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#endif
+        uint32_t* gh = ctl + RS_HREP + (p * RS_NG + tr.grp) * HBINS;
+        for (int i = t; i < HBINS; i += RS_NT)
+            if (h[i]) __hip_atomic_fetch_add(gh + i, h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ++bar;
+        if (rs_arrive(tr, &flag_s, &gen_s, gen)) {
+            // the merger: the replicas summed, the digit picked, the result released with the
+            // generation; the replicas cleared for the next call after that (off the critical path)
+            RS_STAMP(2 + 3 * p);
+            uint32_t* r0 = ctl + RS_HREP + p * RS_NG * HBINS;
+            for (int i = t; i < HBINS; i += RS_NT) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int r = 0; r < RS_NG; ++r) c += __hip_atomic_load(r0 + r * HBINS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                h[i] = (i == 0 && prefix == 0u) ? c - pad : c;
+            }
+            __syncthreads();
+            uint32_t bin, above;
+            hist_find(h, krem, bin, above, scratch);
+            const uint32_t lst = h[bin];
+            rs_release(tr, &gen_s, bin, above, lst);
+            if (t == 0) { scratch[0] = bin; scratch[1] = above; scratch[2] = lst; }
+            for (int i = t; i < HBINS; i += RS_NT)
+#pragma unroll
+                for (int r = 0; r < RS_NG; ++r) __hip_atomic_store(r0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            RS_STAMP(2 + 3 * p);
+            rs_wait(tr, &gen_s, scratch);
+        }
+        __syncthreads();
+        const uint32_t bin = scratch[0], above = scratch[1];
+        last = scratch[2];
+        prefix = (prefix << pass_bits(p)) | bin;
+        krem -= above;
+        __syncthreads();
+        RS_STAMP(3 + 3 * p);
+        if (p == 1 && last <= (uint32_t)RS_CAP) { cand = true; break; }  // (uniform) the candidate finish
+    }
+    if (cand) {
+        // Candidate finish (after two digits, the K-th key's 22-bit prefix P holding <= RS_CAP
+        // elements): keys above P are kept, below dropped, and the elements AT P — the K-th and its
+        // equals — are stored as +0 now and listed (value bits, index); the last workgroup to arrive
+        // ranks the list by (key desc, tie order), stores the krem first and writes the row state.
+        // The third digit's round and the tie counts' exchange are not needed; nobody waits for the
+        // ranking.  (The padding of the straddling float4 is never listed.)
+        const uint32_t P = prefix;
+        uint32_t nc = 0;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            if (u < uv) {
+                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    nc += ((mag_key(e[q]) >> 9) == P && (int64_t)(f0 + u * RS_NT) * 4 + q < d) ? 1u : 0u;
+            }
+        }
+        uint32_t ctot;
+        uint32_t pos = ex_scan<RS_NT>(nc, wsum, ctot);
+        if (ctot) {                                                      // (uniform)
+            if (t == 0) scratch[0] = __hip_atomic_fetch_add(ctl + RS_CCNT, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            pos += scratch[0];
+        }
+        uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            if (u < uv) {
+                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                uint32_t o[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t kp = mag_key(e[q]) >> 9;
+                    const uint32_t j = (f0 + u * RS_NT) * 4u + (uint32_t)q;
+                    o[q] = kp > P ? __float_as_uint(e[q]) : 0u;
+                    if (kp == P && (int64_t)j < d) {
+                        if (pos < (uint32_t)RS_CAP)
+                            __hip_atomic_store(cl + pos, ((uint64_t)__float_as_uint(e[q]) << 32) | j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ++pos;
+                    }
+                }
+                const u4v ov = {o[0], o[1], o[2], o[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, 0);
+            }
+        }
+        RS_STAMP(10);
+        if (rs_arrive(tr, &flag_s, &gen_s, 0u)) {
+            // the last workgroup: rank the m listed elements, keep the krem first
+            __shared__ uint64_t comp[RS_CAP];
+            __shared__ uint64_t kth_s;
+            const uint32_t m = __hip_atomic_load(ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool ok = m == last && m >= krem && krem >= 1u;          // every element at P listed
+            const uint32_t mm = min(m, (uint32_t)RS_CAP);
+            for (uint32_t i = t; i < mm; i += RS_NT) {
+                const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                comp[i] = ((uint64_t)((uint32_t)(en >> 32) & 0x7FFFFFFFu) << 32) | tie_pref((uint32_t)en, ws.tie_hi);
+            }
+            if (t == 0) { scratch[2] = 0; scratch[3] = 0; kth_s = ~0ull; }
+            __syncthreads();
+            if (ok)
+                for (uint32_t i = t; i < mm; i += RS_NT) {
+                    const uint64_t me = comp[i];
+                    uint32_t rank = 0;
+                    for (uint32_t jj = 0; jj < mm; ++jj) rank += comp[jj] > me ? 1u : 0u;
+                    if (rank == krem - 1u) kth_s = me;                   // entries are distinct
+                }
+            __syncthreads();
+            const uint64_t kc = kth_s;
+            const uint32_t kth = (uint32_t)(kc >> 32);
+            if (ok)
+                for (uint32_t i = t; i < mm; i += RS_NT) {
+                    const uint64_t me = comp[i];
+                    if (me >= kc) {
+                        const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        out[(uint32_t)en] = __uint_as_float((uint32_t)(en >> 32));
+                    }
+                    const uint32_t key = (uint32_t)(me >> 32);
+                    if (key > kth) atomicAdd(&scratch[2], 1u);
+                    else if (key == kth) atomicAdd(&scratch[3], 1u);
+                }
+            __syncthreads();
+            if (t == 0) {
+                __hip_atomic_store(ctl + RS_CCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // clean for the next call
+                const uint32_t gt = scratch[2], eq = scratch[3];
+                const bool gave_up = __hip_atomic_exchange(ctl + RS_GAVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                ws.thr[0] = kth;
+                ws.krem[0] = krem - gt;
+                ws.tiecut[0] = tie_pref((uint32_t)kc, ws.tie_hi);
+                ws.flags[0] = F_RESIDENT | (gt + eq > krem ? F_TIES : 0u) | ((gave_up || !ok) ? F_OVERFLOW : 0u);
+            }
+        }
+        RS_STAMP(11);
+    } else {
+    // thr = the K-th key; krem of the `last` elements equal to it are kept
+    const uint32_t thr = prefix;
+    const bool tie_cut = last > krem;                                    // uniform over the grid
+    uint64_t tmask = 0;                                                  // kept ties: bit 4 u + q
+    if (tie_cut) {
+        // this workgroup's ties (its padding, at its end, is not one), published as (call seq << 32 |
+        // count); a workgroup holding ties sums the counts of the workgroups before it (waiting for
+        // each to be published: all publish right after the last digit, so no barrier round) and
+        // ranks its own in (u, t, q) order; the others have nothing to rank
+        uint32_t c = 0;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            if (u < uv) {
+                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c += mag_key(e[q]) == thr ? 1u : 0u;
+            }
+        }
+        uint32_t tot;
+        (void)ex_scan<RS_NT>(c, wsum, tot);
+        if (thr == 0u && g == padg) tot -= pad;
+        uint64_t* tc = reinterpret_cast<uint64_t*>(ctl + RS_TCNT);
+        if (t == 0) __hip_atomic_store(tc + g, ((uint64_t)seq << 32) | tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tot == 0u) goto store;                                       // (uniform) no tie here
+        uint32_t part = 0, run = 0;
+        for (uint32_t i = t; i < g; i += RS_NT) {
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            uint64_t w;
+            while ((uint32_t)((w = __hip_atomic_load(tc + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != seq) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((uint64_t)wall_clock64() - t0 > FLC_RS_SPIN) {
+                    __hip_atomic_fetch_or(ctl + RS_GAVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            part += (uint32_t)w;
+        }
+        (void)ex_scan<RS_NT>(part, wsum, run);                           // ties in the workgroups before
+        const uint32_t tie_from = ws.tie_hi ? last - krem : 0u, tie_to = ws.tie_hi ? last : krem;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            if (u < e4) {                                                // (uniform: ex_scan inside)
+                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                uint32_t ce = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ce += (u < uv && mag_key(e[q]) == thr) ? 1u : 0u;
+                uint32_t tu;
+                uint32_t r = run + ex_scan<RS_NT>(ce, wsum, tu);
+                run += tu;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (u < uv && mag_key(e[q]) == thr) {
+                        if (r >= tie_from && r < tie_to) tmask |= 1ull << (4 * u + q);
+                        ++r;
+                    }
+            }
+        }
+    }
+store:
+    RS_STAMP(10);
+    // the dense output from the registers: x where kept, +0 elsewhere (range-checked: no padding)
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+        if (u < uv) {
+            const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t k = mag_key(e[q]);
+                const bool keep = k > thr || (k == thr && (!tie_cut || ((tmask >> (4 * u + q)) & 1ull)));
+                o[q] = keep ? __float_as_uint(e[q]) : 0u;
+            }
+            const u4v ov = {o[0], o[1], o[2], o[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, 0);
+        }
+    }
+    RS_STAMP(11);
+    // row state for flc_select_row_flags (every workgroup knows it; workgroup 0 writes it)
+    if (g == 0 && t == 0) {
+        // (a wait that gave up: flagged; the flag is cleared for the next call's report)
+        const bool gave_up = __hip_atomic_exchange(ctl + RS_GAVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        (void)bar;
+        ws.thr[0] = thr;
+        ws.krem[0] = krem;
+        ws.tiecut[0] = 0;
+        ws.flags[0] = F_RESIDENT | (tie_cut ? F_TIES : 0u) | (gave_up ? F_OVERFLOW : 0u);
+    }
+    }
+#ifdef FLC_RS_PRINT
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    RS_STAMP(12);
+    if (g == 0 && t == 0) {
+        const uint64_t* pr = reinterpret_cast<const uint64_t*>(ctl + RS_PROBE);
+        uint64_t smax = 0, amax = 0, smin = ~0ull;
+        uint32_t gs = 0, ga = 0;
+        for (uint32_t i = 0; i < G; ++i) {
+            const uint64_t s0 = __hip_atomic_load(pr + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t a0 = __hip_atomic_load(pr + 1024 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            smin = s0 < smin ? s0 : smin;
+            if (s0 > smax) { smax = s0; gs = i; }
+            if (a0 > amax) { amax = a0; ga = i; }
+        }
+        printf("rs_skew: start spread %llu (last wg %u), last pass-0 hist done at %llu (wg %u, its own %llu) after wg 0 start\n",
+               smax - smin, gs, amax - stamp[0], ga, amax - __hip_atomic_load(pr + ga, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    if (g == 0 && t == 0)
+        printf("rs_stamps G=%u e4=%d NG=%d: load+h0 %llu arrive0 %llu wait0 %llu | h1 %llu arrive1 %llu wait1 %llu | h2 %llu arrive2 %llu wait2 %llu | tie %llu store %llu drain %llu (x10ns)\n",
+               G, e4, RS_NG, stamp[1] - stamp[0], stamp[2] - stamp[1], stamp[3] - stamp[2], stamp[4] - stamp[3], stamp[5] - stamp[4],
+               stamp[6] - stamp[5], stamp[7] - stamp[6], stamp[8] - stamp[7], stamp[9] - stamp[8], stamp[10] - stamp[9],
+               stamp[11] - stamp[10], stamp[12] - stamp[11]);
+#endif
+}
+
 // ------------------------------------------------------------------------------------------
 // Host orchestration
 // ------------------------------------------------------------------------------------------
@@ -2312,6 +2937,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
     SelWs s;
     s.tie_hi = 0;
+    s.lh_stride = 1;
     s.cap = sel_capacity(codec, d, K);
     s.tab = cv.take<uint2>((size_t)C * nn);
     s.ent_idx = cv.take<uint32_t>((size_t)nn * s.cap);
@@ -2329,6 +2955,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tieprefix = cv.take<uint32_t>((size_t)C * nn);
         s.tiecut = cv.take<uint32_t>(nn);
         s.hist = cv.take<uint32_t>((size_t)nn * HBINS);
+        s.lhist = cv.take<uint32_t>((size_t)HBINS * FLC_LONE_HSMAX);
         s.cursor = nullptr;
         s.cstate = cv.take<uint32_t>((size_t)nn * CS_ST);
         s.clist = cv.take<uint64_t>((size_t)std::min<int64_t>(nn, CS_FEW) * CS_LCAP);
@@ -2338,6 +2965,7 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tieprefix = nullptr;
         s.tiecut = nullptr;
         s.hist = nullptr;
+        s.lhist = nullptr;
         s.cursor = cv.take<uint32_t>((size_t)std::max<int64_t>(C, RK_SB) * nn);   // RandK: [N][RK_SB] segment offsets
         s.cstate = nullptr;
         s.clist = nullptr;
@@ -2383,6 +3011,52 @@ static bool cs_single() {            // tuning runs: FLC_CS_SINGLE=1 keeps the o
     return v;
 }
 
+#ifndef FLC_LONE_PATH
+#define FLC_LONE_PATH 2                // a lone compressVector row: 2 in registers (k_lone_resident, rows up to
+#endif                                 // RS_U * 4096 per CU; longer: 0), 1 three launches (k_lone_finish), 0 five
+#ifndef FLC_RS_COOP
+#define FLC_RS_COOP 0                  // 1: k_lone_resident launched cooperatively (HIP's launch: +22 us a call
+#endif                                 // measured; residency holds anyway: G <= CUs, one workgroup per CU, launches serialised)
+// k_lone_resident's control block (library-owned, one per device, zeroed once: the kernel leaves it
+// clean) and the serialisation of its launches: two resident grids at once could each hold part of
+// the chip and wait for the other forever, so a launch on another stream than the previous one
+// waits for that one's completion event (one stream: stream order alone)
+struct RsCtx {
+    uint32_t* ctl = nullptr;
+    uint32_t seq = 0;                   // launches so far (tags the tie counts of each call)
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+};
+static std::mutex g_rs_mu;
+static std::map<int, RsCtx> g_rs_ctx;
+static int rs_cus() {              // compute units of the current device (one k_lone_resident workgroup each)
+    static int cu[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cu[dev]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cu[dev] = c;
+    }
+    return cu[dev];
+}
+static int lone_path() {           // tuning runs: env FLC_LONE_PATH overrides
+    static const int v = [] { const char* e = tuning_env("FLC_LONE_PATH"); return e ? atoi(e) : FLC_LONE_PATH; }();
+    return v;
+}
+
+static bool lone_zs() {           // the short path's output zeros beside the sample (1) or in the filter (0)
+    static const bool v = [] { const char* e = tuning_env("FLC_LONE_ZS"); return e ? atoi(e) != 0 : true; }();
+    return v;
+}
+static uint32_t lone_hs() {
+    static const uint32_t v = [] {
+        const char* e = tuning_env("FLC_LONE_HS");
+        return (uint32_t)std::min<int64_t>(std::max<int64_t>(e ? atoll(e) : FLC_LONE_HS, 1), FLC_LONE_HSMAX);
+    }();
+    return v;
+}
+
 static int filter_group() {
     static const int g = [] {
         const char* e = tuning_env("FLC_FILTER_GS");     // tuning runs only
@@ -2393,7 +3067,7 @@ static int filter_group() {
 
 template <int FGS>
 static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, SelWs ws, hipStream_t st,
-                          int shards, float* zout = nullptr) {
+                          int shards, float* zout = nullptr, int lone = 0) {
     // oversubscribed grid (measured: 16-32 K blocks beat a resident-only persistent grid by ~5 %,
     // the hardware dispatcher balances the tail)
     const int64_t waves = rn * ((nchunks(d) + FGS - 1) / FGS);
@@ -2404,8 +3078,14 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
     ProfScope _pv(FGS == 4 ? "k_topk_filter_g4" : "k_topk_filter_g2", st);   // which variant ran (tests)
-    if (zout)
-        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, true>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
+    if (lone == 2)
+        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, 2>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
+                           std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
+    else if (lone == 3)
+        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, 3>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
+                           std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
+    else if (zout)
+        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, 1>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
     else
         hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
@@ -2610,9 +3290,10 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (codec == FLC_TOPK) {
         if (prm->tie != FLC_TIE_LOWEST && prm->tie != FLC_TIE_HIGHEST) { set_error("topk: unknown tie rule %d", prm->tie); return FLC_ERR_ARG; }
         ws.tie_hi = prm->tie == FLC_TIE_HIGHEST ? 1u : 0u;
+        ws.lh_stride = lone_hs();
     }
     const int64_t C = host_chunks(d);
-    bool lone_assign = false, gfold = false;
+    bool lone_assign = false, lone_short = false, gfold = false;
     // TopK, few rows: sharded candidate lists (k_topk_filter_fast) and the spread select (k_cs_pass)
     const bool few = codec == FLC_TOPK && n <= CS_FEW && !cs_single() && sel_capacity(codec, d, K) >= (int64_t)CS_SH * GCAP;
     if (codec == FLC_RANDK) {
@@ -2633,17 +3314,67 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             FLC_CHECK_LAUNCH("k_randk_fine");
         }
     } else {  // TOPK
+        // a lone compressVector row up to RS_U * 4096 elements per CU (any K): in registers, one launch
+        if (assign && n == 1 && !assign_fold() && lone_path() == 2) {
+            const int64_t cus = rs_cus();
+            const int64_t G = std::min<int64_t>(cus, (d + RS_NT * 4 - 1) / (RS_NT * 4));
+            const int64_t e4 = G > 0 ? (d + G * RS_NT * 4 - 1) / (G * RS_NT * 4) : RS_U + 1;
+            if (e4 <= RS_U && d * 4 < ((int64_t)1 << 31)) {
+                const int64_t Gu = (d + e4 * RS_NT * 4 - 1) / (e4 * RS_NT * 4);   // no workgroup of padding only
+                ProfScope _ps("k_lone_resident", st);
+                int dev = 0;
+                FLC_CHECK_HIP(hipGetDevice(&dev));
+                std::lock_guard<std::mutex> lk(g_rs_mu);
+                RsCtx& rc = g_rs_ctx[dev];
+                if (!rc.ctl) {
+                    FLC_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&rc.ctl), (size_t)RS_CTL * sizeof(uint32_t)));
+                    FLC_CHECK_HIP(hipMemset(rc.ctl, 0, (size_t)RS_CTL * sizeof(uint32_t)));
+                    FLC_CHECK_HIP(hipEventCreateWithFlags(&rc.done, hipEventDisableTiming));
+                }
+                hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+                FLC_CHECK_HIP(hipStreamIsCapturing(st, &cap));
+                if (rc.last && rc.last != st && cap == hipStreamCaptureStatusNone) FLC_CHECK_HIP(hipStreamWaitEvent(st, rc.done, 0));
+                const int e4i = (int)e4;
+                if (FLC_RS_COOP) {
+                    RowSrc ra = rows;
+                    int64_t da = d, ka = K;
+                    SelWs wa = ws;
+                    float* oa = out;
+                    int ea = e4i;
+                    uint32_t* ca = rc.ctl;
+                    uint32_t sa = ++rc.seq;
+                    void* args[] = {&ra, &da, &ka, &wa, &oa, &ea, &ca, &sa};
+                    FLC_CHECK_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_lone_resident<RS_U>), dim3((unsigned)Gu),
+                                                             dim3(RS_NT), args, 0, st));
+                } else {
+                    hipLaunchKernelGGL((k_lone_resident<RS_U>), dim3((unsigned)Gu), dim3(RS_NT), 0, st, rows, d, K, ws, out, e4i, rc.ctl, ++rc.seq);
+                }
+                if (cap == hipStreamCaptureStatusNone) {
+                    FLC_CHECK_HIP(hipEventRecord(rc.done, st));
+                    rc.last = st;
+                }
+                FLC_CHECK_LAUNCH("k_lone_resident");
+                return FLC_OK;
+            }
+        }
         const bool dense_k = K * 16 > d;   // large K: the candidate list would not be smaller than the row
         // a lone compressVector (assign, one row) on the fast path: output zeros from the filter, the
         // exact fallback and the scatter in one launch (k_assign_finish)
         lone_assign = assign && n == 1 && few && !dense_k && !assign_fold();
+        // ... in three launches (k_lone_finish after the filter) unless a tuning run asks for the
+        // five-launch path (k_cs_pass x 2 + k_assign_finish)
+        lone_short = lone_assign && lone_path() == 1;
+
         if (dense_k) FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const int64_t bpr = (C + 3) / 4;
         if (!dense_k) {
             { ProfScope _ps("k_topk_sample", st);
-            // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3)
-            hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
-                               few ? 1 : 0); }
+            // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3);
+            // the short lone-row path: one more workgroup per 16 chunks writes the output's zeros
+            const bool zs = lone_short && lone_zs();
+            const unsigned zb = zs ? (unsigned)((C + 15) / 16) : 0u;
+            hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)n + zb), dim3(1024), 0, st, rows, n, d, K, ws,
+                               few ? 1 : 0, lone_short ? 1 : 0, zs ? out : (float*)nullptr); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             // per row group: filter (the full read), then the candidate select and the exact
             // fallback of the group's rows; with TG > 1 groups the select + fallback of group g run
@@ -2678,9 +3409,11 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 // few rows: 2-chunk groups (twice the waves in flight for a lone row)
                 // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
                 // a lone compressVector row: the filter also writes the dense output's zeros
-                float* zout = lone_assign ? out : nullptr;
-                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout);
-                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout); }
+                // (the short path: zeros here unless beside the sample, + the first-digit histogram)
+                float* zout = lone_assign && !(lone_short && lone_zs()) ? out : nullptr;
+                const int lone = lone_short ? (zout ? 3 : 2) : 0;
+                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout, lone);
+                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout, lone); }
                 FLC_CHECK_LAUNCH("k_topk_filter");
                 if (TG > 1) {
                     FLC_CHECK_HIP(hipEventRecord(cx->ev[g], st));
@@ -2692,7 +3425,9 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 // settle a row whose first digit's bin holds <= CS_LCAP entries (~(4 sqrt(ks) + 8)
                 // D / 16 K spread over 256-512 bins: up to ~900 at D = 64 M), else 3 cover every
                 // shift; many rows: 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
-                if (few) {
+                if (lone_short) {
+                    // the digit, its bin's ranking and the scatter: k_lone_finish below
+                } else if (few) {
                     const int np = (FLC_CS_LIST && d <= FLC_CS_TWO_MAXD) ? 2 : 3;
                     for (int p = 0; p < np; ++p)
                         hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws,
@@ -2776,6 +3511,13 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
+    if (lone_short) {
+        ProfScope _ps("k_lone_finish", st);
+        if (vec) hipLaunchKernelGGL((k_lone_finish<true>), dim3(CS_SH), dim3(EX_NT), 0, st, rows, d, K, ws, out);
+        else hipLaunchKernelGGL((k_lone_finish<false>), dim3(CS_SH), dim3(EX_NT), 0, st, rows, d, K, ws, out);
+        FLC_CHECK_LAUNCH("k_lone_finish");
+        return FLC_OK;
+    }
     if (lone_assign) {
         // output zeros written by the filter; exact fallback (if the row failed) + scatter
         ProfScope _ps("k_assign_finish", st);

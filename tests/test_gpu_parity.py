@@ -382,11 +382,10 @@ def test_topk_few_rows_kth_ties_vs_oracle(ag, d):
 @pytest.mark.parametrize("kind", ["normal", "heavy", "ties", "zeros", "clustered", "nan_inf", "fewnz"])
 @pytest.mark.parametrize("d,k", [((1 << 21) + 3, 20_000), (10_000_000, 100_000), (4_000_000, 80_000)])
 def test_topk_lone_row_vs_oracle(ag, kind, d, k):
-    """A lone compressVector row (compressors.py:330-335) on its own pipeline: the sample, the
-    filter into 64 list shards that also zeroes the output, the candidate select spread over the
-    shards (k_cs_pass, one launch per digit) and k_assign_finish (the exact fallback or the
-    scatter).  Bit-exact vs the oracle (lowest-index ties); the Gaussian rows stay off the exact
-    path."""
+    """A lone compressVector row (compressors.py:330-335) on its own pipeline: up to 16.7 M
+    elements held in the chip's registers (k_lone_resident: exact radix select with grid barriers,
+    the dense output written from the registers; flag 16).  Bit-exact vs the oracle (lowest-index
+    ties) on every kind; never the exact fallback."""
     g = np.random.default_rng([d, k, len(kind)])
     x = _topk_rows(kind, 1, d, g)[0]
     want = _topk_enc([x], k)[0]
@@ -394,8 +393,7 @@ def test_topk_lone_row_vs_oracle(ag, kind, d, k):
     xt = torch.from_numpy(x).cuda()
     assert_bitexact(c.compressVector(xt), want)
     f = int(ag.select_row_flags(c, 1, d)[0])
-    if kind in ("normal", "heavy"):
-        assert f & 8 == 0, f"flags {f}: the row took the exact path"
+    assert f & 16 and f & 8 == 0 and f & 1 == 0, f"flags {f}: expected the register-resident select"
     # the same row at a 4-byte offset (scalar loads; the exact fallback's non-vector variant)
     buf = torch.zeros(d + 1, device="cuda")
     buf[1:] = xt
@@ -419,11 +417,10 @@ def test_topk_lone_row_three_passes(ag, kind):
 
 @pytest.mark.parametrize("ties", [20, 600, 1500, 3000])
 def test_topk_lone_row_tie_capacity(ag, ties):
-    """The lone row's tie cut (k_cs_pass's last arriver gathers the indices of the entries equal to
-    the K-th key over all shards, at most TIECAP = 2048 of them, and admits the lowest): `ties`
-    extra entries equal to the K-th magnitude (signs mixed, spread over the row) straddle the cut.
-    Up to 1500 the fast path settles it (F_TIES set, no exact path); 3000 take the exact path.
-    Bit-exact vs the oracle either way."""
+    """The lone row's tie cut: `ties` extra entries equal to the K-th magnitude (signs mixed, spread
+    over the row) straddle the cut.  The register-resident select (flag 16) ranks them over the grid
+    whatever their number (F_TIES set, no exact path); the list path's TIECAP = 2048 bound (k_cs_pass)
+    applies to rows longer than 16.7 M only.  Bit-exact vs the oracle."""
     d, k = 4_000_000, 40_000
     g = np.random.default_rng([ties, 3])
     x = g.standard_normal(d).astype(np.float32)
@@ -436,10 +433,7 @@ def test_topk_lone_row_tie_capacity(ag, ties):
     c = ag.initCompressor(f"topk:{k}", d)
     assert_bitexact(c.compressVector(torch.from_numpy(x).cuda()), want)
     f = int(ag.select_row_flags(c, 1, d)[0])
-    if ties <= 1500:
-        assert f & 8 == 0 and f & 4, f"flags {f}: expected the fast path's tie cut"
-    else:
-        assert f & 8, f"flags {f}: expected the exact path"
+    assert f & 16 and f & 4 and f & 8 == 0, f"flags {f}: expected the resident select's tie cut"
 
 
 def test_topk_few_rows_stay_on_fast_path(ag):

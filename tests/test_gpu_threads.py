@@ -110,3 +110,41 @@ def test_one_thread_two_streams_interleaved():
         for ot, oq in outs:
             assert np.array_equal(ot.cpu().numpy().view(np.uint32), want["topk:1%"].view(np.uint32))
             assert np.array_equal(oq.cpu().numpy().view(np.uint32), want["qsgd:127"].view(np.uint32))
+
+
+def test_resident_compressvector_threads_distinct_streams():
+    """The register-resident lone TopK select (k_lone_resident) needs its whole grid on the chip at
+    once; two of its grids running together could each hold part of it and wait for the other.  Its
+    launches are serialised across streams (each waits for the previous one's completion event), so
+    four host threads on four streams calling compressVector at once all finish, bit-exact vs the
+    same call alone, with no barrier giving up (flag 1)."""
+    from flpytorch_amd import aggregation as ag
+    d = 4_000_003
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xs = [torch.randn(d, generator=g, device="cuda") for _ in range(4)]
+    want = [ag.initCompressor("topk:1%", d).compressVector(x).clone() for x in xs]
+    torch.cuda.synchronize()
+    got, errors = [None] * 4, []
+
+    def worker(i):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                c = ag.initCompressor("topk:1%", d)
+                outs = [c.compressVector(xs[i]) for _ in range(5)]
+                f = int(ag.select_row_flags(c, 1, d)[0])
+            s.synchronize()
+            got[i] = ([o.clone() for o in outs], f)
+        except Exception as e:          # surfaced below
+            errors.append((i, repr(e)))
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    for i in range(4):
+        outs, f = got[i]
+        assert f & 16 and not f & 1, f"thread {i}: flags {f}"
+        for o in outs:
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), want[i].cpu().numpy().view(np.uint32))

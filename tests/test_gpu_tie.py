@@ -111,8 +111,9 @@ def test_fused_exact_fallback_tie_rules(ag, kind):
 
 @pytest.mark.parametrize("d,k,ties", [(2_000_003, 20_000, 40), (10_000_000, 100_000, 600), (4_000_000, 40_000, 3000)])
 def test_compressvector_tie_rules(ag, d, k, ties):
-    """A lone compressVector row (the drop-in): the spread select's tie cut (k_cs_pass) up to TIECAP
-    ties, the exact path (k_assign_finish's exact_row) beyond it."""
+    """A lone compressVector row (the drop-in), D <= 16.7 M: the register-resident exact select
+    (k_lone_resident, flag 16) ranks the ties at the K-th key over the whole grid, any number of
+    them, under either rule (F_TIES set, never the exact fallback)."""
     g = np.random.default_rng([d, ties])
     x = g.standard_normal(d).astype(np.float32)
     mags = np.sort(np.abs(x))[::-1]
@@ -128,7 +129,7 @@ def test_compressvector_tie_rules(ag, d, k, ties):
         want = _enc([x], k, tie)[0]
         np.testing.assert_array_equal(_bits(outs[tie]), _bits(want))
         f = int(ag.select_row_flags(c, 1, d)[0])
-        assert (f & 8) if ties > 2048 else (f & 4 and not f & 8), f"{tie}: flags {f}"
+        assert f & 16 and f & 4 and not f & 8, f"{tie}: flags {f}"
     assert not np.array_equal(_bits(outs["lowest"]), _bits(outs["highest"]))
 
 
@@ -157,3 +158,29 @@ def test_tie_rule_validation(ag):
     c.tie_policy = "middle"
     with pytest.raises(ValueError):
         c.codec_params(torch.device("cuda"))
+
+
+@pytest.mark.parametrize("d", [2_000_003, 4_000_001, 10_000_000, 16_777_216, 16_777_217, 1_000])
+@pytest.mark.parametrize("kind", ["fewnz", "ties", "normal"])
+def test_compressvector_resident_edges(ag, d, kind):
+    """The register-resident lone select (k_lone_resident) at its edges: rows whose length is not a
+    multiple of 4 (the padding of the straddling float4 is +0, at the end of the index order, and must
+    neither count nor be kept when the K-th magnitude is 0: fewnz under the highest-index rule), a
+    row of exactly 16 float4 x 4096 x 256 elements and one past it (the list path), and a tiny row
+    with K above D / 16 (one workgroup).  Both tie rules, bit-exact vs the oracle."""
+    g = np.random.default_rng([d, len(kind)])
+    k = max(1, d // 100) if d > 10_000 else 300
+    x = g.standard_normal(d).astype(np.float32)
+    if kind == "fewnz":
+        x[np.argsort(g.random(d))[: d - k // 3]] = 0.0             # fewer nonzeros than K: zeros tie
+    elif kind == "ties":
+        x = _straddle(x[None, :].copy(), k, g)[0]
+    xt = torch.from_numpy(x).cuda()
+    for tie in ("lowest", "highest"):
+        c = _comp(ag, f"topk:{k}", d, tie)
+        got = c.compressVector(xt)
+        np.testing.assert_array_equal(_bits(got), _bits(_enc([x], k, tie)[0]), err_msg=f"{tie}")
+        f = int(ag.select_row_flags(c, 1, d)[0])
+        assert not f & 1, f"{tie}: flags {f} (a barrier gave up)"
+        if d <= 16_777_216 and d * 4 < 2**31:
+            assert f & 16, f"{tie}: flags {f}, expected the register-resident select"

@@ -1,8 +1,8 @@
 #!/bin/bash
-# copy an evidence pass (tools/gpu/evidence_r04.sh, gpurun_out/<ev>) into profiles/r04/<dst>
+# copy an evidence pass (tools/gpu/evidence_r04.sh, gpurun_out/<ev>) into profiles/${ROUND:-r05}/<dst>
 # usage: tools/collect_final.sh <ev> <dst> "<build note>"
 set -e
-src=gpurun_out/$1; dst=profiles/r04/$2; mkdir -p $dst
+src=gpurun_out/$1; dst=profiles/${ROUND:-r05}/$2; mkdir -p $dst
 for f in $src/bench_*.log $src/dropin_*.log $src/e2e_*.log; do
   b=$(basename $f .log); grep '^{' $f | tail -1 > $dst/$b.jsonl
 done
