@@ -56,8 +56,13 @@ constexpr int RS_NG = FLC_RS_NG;
 // its control words: counters on lines of their own, per-group digit histograms, tie counts
 constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128;
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
+constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
+#ifndef FLC_RS_SPEC
+#define FLC_RS_SPEC 1                 // k_lone_resident: speculative first digit (two digits in one round)
+#endif
 constexpr int RS_HREP = RS_GRP + 32 * RS_NG;
-constexpr int RS_CLIST = RS_HREP + 3 * RS_NG * HBINS;    // [RS_CAP] (value bits, index)
+constexpr int RS_HSPEC = RS_HREP + 3 * RS_NG * HBINS;    // [RS_NG][3][HBINS] speculative second digit
+constexpr int RS_CLIST = RS_HSPEC + 3 * RS_NG * HBINS;   // [RS_CAP] (value bits, index)
 constexpr int RS_TCNT = RS_CLIST + 2 * RS_CAP;
 #ifdef FLC_RS_PRINT
 constexpr int RS_PROBE = RS_TCNT + 2048;   // probe builds: per-workgroup start / arrival stamps
@@ -2525,11 +2530,11 @@ struct RsTree {
     uint32_t* ctl;
     uint32_t grp, gsz, ngr;             // this workgroup's group, its size, groups in use
 };
-// The release word (64 bits at RS_GEN): generation mod 16 | the digit's bin << 4 | the count above it
-// << 15 (24 bits: < K <= 2^24) | the bin's count << 39 (25 bits): the waiters get the merger's result
-// with the release itself.
-__device__ inline uint64_t rs_word(uint32_t gen, uint32_t bin, uint32_t above, uint32_t last) {
-    return (uint64_t)(gen & 15u) | ((uint64_t)bin << 4) | ((uint64_t)above << 15) | ((uint64_t)last << 39);
+// The release word (64 bits at RS_GEN): generation mod 8 | a 61-bit payload, the merger's result, so
+// that the waiters get it with the release itself.  A digit's payload: bin | the count above it << 11
+// (24 bits: < K <= 2^24) | the bin's count << 35 (25 bits).
+__device__ inline uint64_t rs_digit(uint32_t bin, uint32_t above, uint32_t last) {
+    return (uint64_t)bin | ((uint64_t)above << 11) | ((uint64_t)last << 35);
 }
 // Self-resetting two-level barrier (no per-call clearing): a group's counter is reset by its last
 // arriver, the global one by the last group's; every workgroup reads the release word BEFORE
@@ -2539,7 +2544,7 @@ __device__ inline uint64_t rs_word(uint32_t gen, uint32_t bin, uint32_t above, u
 // (gen: the release word's generation, read by thread 0 before this workgroup's flush — any time
 // after the previous release — so that its load is not one more round trip here)
 __device__ inline uint32_t rs_gen(const RsTree& tr) {
-    return (uint32_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 15u;
+    return (uint32_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 7u;
 }
 __device__ inline bool rs_arrive(const RsTree& tr, uint32_t* flag_s, uint32_t* gen_s, uint32_t gen) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                     // this wave's atomics performed
@@ -2564,22 +2569,22 @@ __device__ inline bool rs_arrive(const RsTree& tr, uint32_t* flag_s, uint32_t* g
     return *flag_s != 0u;
 }
 // the merger, after its writes: the release word with its result
-__device__ inline void rs_release(const RsTree& tr, const uint32_t* gen_s, uint32_t bin, uint32_t above, uint32_t last) {
+__device__ inline void rs_release(const RsTree& tr, const uint32_t* gen_s, uint64_t payload) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(tr.ctl + RS_GEN), rs_word(*gen_s + 1u, bin, above, last), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(tr.ctl + RS_GEN), (uint64_t)((*gen_s + 1u) & 7u) | (payload << 3),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-// everyone else: the release word (thread 0 leaves it in res_s[0..2] = bin, above, last)
+// everyone else: the release word (thread 0 leaves its payload in res_s[0..1], low word first)
 __device__ inline void rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t* res_s) {
     if (threadIdx.x == 0) {
         const uint64_t* rw = reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN);
         const uint64_t t0 = (uint64_t)wall_clock64();
         uint64_t w;
-        while (((uint32_t)(w = __hip_atomic_load(rw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 15u) == *gen_s) {
+        while (((uint32_t)(w = __hip_atomic_load(rw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 7u) == *gen_s) {
             __builtin_amdgcn_s_sleep(1);
             if ((uint64_t)wall_clock64() - t0 > FLC_RS_SPIN) {
                 __hip_atomic_fetch_or(tr.ctl + RS_GAVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2587,9 +2592,8 @@ __device__ inline void rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        res_s[0] = (uint32_t)(w >> 4) & 0x7FFu;
-        res_s[1] = (uint32_t)(w >> 15) & 0xFFFFFFu;
-        res_s[2] = (uint32_t)(w >> 39);
+        res_s[0] = (uint32_t)(w >> 3);
+        res_s[1] = (uint32_t)(w >> 35);
     }
     __syncthreads();
 }
@@ -2634,17 +2638,134 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     const uint32_t pad = (uint32_t)((4 - (d & 3)) & 3);
     const uint32_t padg = (uint32_t)((d / 4) / ((int64_t)e4 * RS_NT));  // the workgroup holding it
     const uint32_t voff = f0 * 16u;
+    // the speculative first digit (rows of >= 4 RS_SS elements): a fixed sample of RS_SS elements
+    // (32 spread pieces of 256), the same in every workgroup, loaded BEFORE the row so that it lands
+    // first (vmcnt retires in order) and its digit is picked while the row streams in
+    const bool spec = FLC_RS_SPEC && d >= 4 * (int64_t)RS_SS;
+    float4 sq0 = make_float4(0.f, 0.f, 0.f, 0.f), sq1 = sq0;
+    if (spec) {
+        const int64_t pos = (int64_t)(t >> 5) * (d - 256) / 31 + (int64_t)(t & 31) * 8;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)(pos * 4), 0, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)(pos * 4 + 16), 0, 0);
+        sq0 = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
+        sq1 = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+    }
+    // the workgroup's part through a descriptor of its own extent: the loads past it (u >= e4, the
+    // row end) return zeros without touching memory, so all RU are issued unconditionally and the
+    // compiler's in-order vmcnt count stays exact (the sample's wait does not drain the row)
+    const int64_t gb = (int64_t)g * e4 * RS_NT * 4;
+    const auto rxg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(0)) + gb, (short)0,
+                                                       (int)(min((int64_t)e4 * RS_NT * 4, d - gb) * 4), 0x00020000);
     float4 v[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-        if (u < uv) {
-            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rx, voff, u * RS_NT * 16, FLC_LOADPOL);
-            v[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
-        }
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rxg, t * 16u, u * RS_NT * 16, FLC_LOADPOL);
+        v[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
     }
     uint32_t prefix = 0, krem = (uint32_t)K, last = 0, bar = 0;
     bool cand = false;
-    for (int p = 0; p < 3; ++p) {
+    uint32_t bs = 0;
+    int p0 = 0;
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    if (spec) {
+        __shared__ uint32_t h1[3 * HBINS];
+        const uint32_t gen = t == 0 ? rs_gen(tr) : 0u;
+        for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
+        for (int i = t; i < 3 * HBINS; i += RS_NT) h1[i] = 0;
+        __syncthreads();
+        {
+            const float e[8] = {sq0.x, sq0.y, sq0.z, sq0.w, sq1.x, sq1.y, sq1.z, sq1.w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) atomicAdd(&h[mag_key(e[q]) >> 20], 1u);
+        }
+        __syncthreads();
+        uint32_t ab;
+        const uint32_t rs = (uint32_t)min((int64_t)RS_SS, max((int64_t)1, (K * RS_SS + d / 2) / d));
+        hist_find(h, rs, bs, ab, scratch);                               // the sample's digit (uniform)
+        for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
+        __syncthreads();
+        // the first digit's histogram, and the second digit's for the first digits bs - 1 .. bs + 1
+        uint32_t km = 0x7FFFFFFFu;
+        asm volatile("" : "+s"(km));
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            if (u < uv) {
+                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t k = __float_as_uint(e[q]) & km;
+                    const uint32_t b0 = k >> 20, w = b0 - bs + 1u;
+                    atomicAdd(&h[b0], 1u);
+                    if (w < 3u) atomicAdd(&h1[w * HBINS + ((k >> 9) & 0x7FFu)], 1u);
+                }
+            }
+        }
+        __syncthreads();
+        RS_STAMP(1);
+        uint32_t* gh = ctl + RS_HREP + tr.grp * HBINS;
+        uint32_t* gs = ctl + RS_HSPEC + tr.grp * 3 * HBINS;
+        for (int i = t; i < HBINS; i += RS_NT)
+            if (h[i]) __hip_atomic_fetch_add(gh + i, h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = t; i < 3 * HBINS; i += RS_NT)
+            if (h1[i]) __hip_atomic_fetch_add(gs + i, h1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ++bar;
+        if (rs_arrive(tr, &flag_s, &gen_s, gen)) {
+            // the merger: the first digit exact; if it is among the three speculated, the second
+            // from the speculative replicas — both digits in ONE round (else the next round takes it)
+            RS_STAMP(2);
+            uint32_t* r0 = ctl + RS_HREP;
+            uint32_t* s0 = ctl + RS_HSPEC;
+            for (int i = t; i < HBINS; i += RS_NT) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int r = 0; r < RS_NG; ++r) c += __hip_atomic_load(r0 + r * HBINS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                h[i] = i == 0 ? c - pad : c;
+            }
+            __syncthreads();
+            uint32_t b0, a0;
+            hist_find(h, (uint32_t)K, b0, a0, scratch);
+            const uint32_t l0 = h[b0], w0 = b0 - bs + 1u;
+            uint64_t pl;
+            if (w0 < 3u) {                                               // (uniform) hit
+                for (int i = t; i < HBINS; i += RS_NT) {
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int r = 0; r < RS_NG; ++r)
+                        c += __hip_atomic_load(s0 + (r * 3 + w0) * HBINS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    h[i] = (i == 0 && b0 == 0u) ? c - pad : c;
+                }
+                __syncthreads();
+                uint32_t b1, a1;
+                hist_find(h, (uint32_t)K - a0, b1, a1, scratch);
+                // hit | 22-bit prefix << 1 | krem << 23 | the prefix's count (saturated) << 47
+                pl = 1ull | ((uint64_t)((b0 << 11) | b1) << 1) | ((uint64_t)((uint32_t)K - a0 - a1) << 23) |
+                     ((uint64_t)min(h[b1], 16383u) << 47);
+            } else {
+                pl = ((uint64_t)b0 << 1) | ((uint64_t)((uint32_t)K - a0) << 23) | ((uint64_t)min(l0, 16383u) << 47);
+            }
+            rs_release(tr, &gen_s, pl);
+            if (t == 0) { scratch[0] = (uint32_t)pl; scratch[1] = (uint32_t)(pl >> 32); }
+            for (int i = t; i < HBINS; i += RS_NT) {                     // clean for the next call
+#pragma unroll
+                for (int r = 0; r < RS_NG; ++r) __hip_atomic_store(r0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int r = 0; r < 3 * RS_NG; ++r) __hip_atomic_store(s0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            RS_STAMP(2);
+            rs_wait(tr, &gen_s, scratch);
+        }
+        __syncthreads();
+        const uint64_t pl = ((uint64_t)scratch[1] << 32) | scratch[0];
+        __syncthreads();
+        prefix = (uint32_t)(pl >> 1) & 0x3FFFFFu;
+        krem = (uint32_t)(pl >> 23) & 0xFFFFFFu;
+        last = (uint32_t)(pl >> 47);
+        p0 = (pl & 1u) ? 2 : 1;
+        cand = p0 == 2 && last <= (uint32_t)RS_CAP;
+        RS_STAMP(3);
+    }
+    for (int p = p0; p < 3 && !cand; ++p) {
         const uint32_t gen = t == 0 ? rs_gen(tr) : 0u;                   // (in flight under the histogram)
         for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
         __syncthreads();
@@ -2690,9 +2811,9 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             __syncthreads();
             uint32_t bin, above;
             hist_find(h, krem, bin, above, scratch);
-            const uint32_t lst = h[bin];
-            rs_release(tr, &gen_s, bin, above, lst);
-            if (t == 0) { scratch[0] = bin; scratch[1] = above; scratch[2] = lst; }
+            const uint64_t pl = rs_digit(bin, above, h[bin]);
+            rs_release(tr, &gen_s, pl);
+            if (t == 0) { scratch[0] = (uint32_t)pl; scratch[1] = (uint32_t)(pl >> 32); }
             for (int i = t; i < HBINS; i += RS_NT)
 #pragma unroll
                 for (int r = 0; r < RS_NG; ++r) __hip_atomic_store(r0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2701,8 +2822,9 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             rs_wait(tr, &gen_s, scratch);
         }
         __syncthreads();
-        const uint32_t bin = scratch[0], above = scratch[1];
-        last = scratch[2];
+        const uint64_t pl = ((uint64_t)scratch[1] << 32) | scratch[0];
+        const uint32_t bin = (uint32_t)pl & 0x7FFu, above = (uint32_t)(pl >> 11) & 0xFFFFFFu;
+        last = (uint32_t)(pl >> 35);
         prefix = (prefix << pass_bits(p)) | bin;
         krem -= above;
         __syncthreads();
@@ -2735,7 +2857,6 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             pos += scratch[0];
         }
         uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
-        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             if (u < uv) {
@@ -2865,7 +2986,6 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
 store:
     RS_STAMP(10);
     // the dense output from the registers: x where kept, +0 elsewhere (range-checked: no padding)
-    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
         if (u < uv) {
