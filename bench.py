@@ -487,11 +487,22 @@ def dropin(args):
         if cnt:
             per_kernel[k] = round(ms / cnt * 1e3, 2)
     cv = rate(cv_bytes, cv_ms)
+    # PMC traffic of the compressVector kernel (tools/collect_pmc.py --dropin), when its pass is on file
+    cv_traffic, cv_kernel = None, None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_dropin_{args.workload}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            pj = json.load(f)
+        cv_kernel = pj.get("kernel")
+        if cv_kernel and any(cv_kernel in k for k in per_kernel):
+            cv_traffic = pj.get("hbm_bytes_per_launch")
     print(json.dumps({"metric": "drop-in compressVector + serverGradient fold, device time; % HBM peak",
                       "mode": "drop-in path (compressVector per client + serverGradient fold) vs fused uplink",
                       "codec": spec, "clients": n, "D": d,
                       "roofline": {"bound": "hbm", "kernel": "compressVector (one row)", "achieved": cv["GBps"],
-                                   "peak": PEAK_GBS, "unit": "GB/s", "frac": cv["frac"], "traffic": None,
+                                   "peak": PEAK_GBS, "unit": "GB/s", "frac": cv["frac"], "traffic": cv_traffic,
+                                   "traffic_unit": "HBM bytes per launch of " + str(cv_kernel) + " (rocprofv3 PMC, profiles/)",
+                                   "traffic_over_algorithmic": round(cv_traffic / cv_bytes, 4) if cv_traffic else None,
                                    "bytes_per_call": cv_bytes, "us_per_call": round(cv_ms * 1e3, 2),
                                    "per_kernel_us": per_kernel,
                                    "bytes_note": "read x + write the dense output (8 D)"

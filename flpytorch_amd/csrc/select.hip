@@ -73,12 +73,6 @@ constexpr int RS_CTL = RS_TCNT + 2048;     // (tie counts: 64-bit (call << 32 | 
 #ifndef FLC_CS_LIST
 #define FLC_CS_LIST 1
 #endif
-#ifndef FLC_LONE_HSMAX
-#define FLC_LONE_HSMAX 1             // largest lone-row histogram stride (words) the workspace holds
-#endif
-#ifndef FLC_LONE_HS
-#define FLC_LONE_HS 1                 // its stride (1: contiguous; 32 / 64 / 1056 measured no different)
-#endif
 #ifndef FLC_CS_TWO_MAXD
 #define FLC_CS_TWO_MAXD (int64_t(64) << 20)   // rows up to this long: two k_cs_pass launches
 #endif
@@ -107,8 +101,6 @@ struct SelWs {            // carved from the caller workspace
     float* part;          // [D] TopK row-group folds: the running tiles carried from one group to the next
     int64_t cap;
     uint32_t tie_hi;      // TopK ties at the K-th key: 0 the lowest indices are kept (default), 1 the highest
-    uint32_t* lhist;      // [HBINS * FLC_LONE_HSMAX] a lone row's first-digit histogram (k_lone_finish path), bin b
-    uint32_t lh_stride;   // at word b * lh_stride (spread over memory channels: its atomics come from every CU)
 };
 
 // Tie order of TopK (flc_codec_params.tie): tie_pref(ix) is larger for the index kept first among
@@ -199,30 +191,13 @@ __device__ inline uint32_t key_bin(uint32_t key, int p) {
 // ------------------------------------------------------------------------------------------
 // DUAL (few rows: latency-bound): the two rank searches share their passes over the sample; the
 // second histogram costs 8 KB of LDS, which would halve the workgroups per CU of a many-row launch.
-// zout (a lone compressVector row, k_lone_finish path): the workgroups past the n sample ones write
-// the dense output's zeros, one wave per 4096-element chunk (the chip is idle beside the one
-// latency-bound sample workgroup; the filter then only reads)
 template <int NT, bool DUAL>
-__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few,
-                                                    int lone, float* __restrict__ zout) {
+__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few) {
     __shared__ uint32_t keys[SMAX];
     __shared__ uint32_t h[HBINS], h2[DUAL ? HBINS : 1];
     __shared__ uint32_t scratch[260], scratch2[DUAL ? 260 : 1];
     const int64_t row = blockIdx.x;
-    if (row >= n) {
-        if (!zout) return;
-        constexpr int WPB = NT / 64;
-        const int lane = threadIdx.x & 63;
-        const int64_t C = nchunks(d), wstride = (int64_t)(gridDim.x - n) * WPB;
-        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-        const u4v z = {0u, 0u, 0u, 0u};
-        for (int64_t c = (row - n) * WPB + (threadIdx.x >> 6); c < C; c += wstride) {
-            const auto ro = chunk_rsrc(zout, c * CHUNK, d);                 // range-checked: the last chunk
-#pragma unroll
-            for (int L = 0; L < 16; ++L) __builtin_amdgcn_raw_buffer_store_b128(z, ro, lane * 16, L * 1024, 0);
-        }
-        return;
-    }
+    if (row >= n) return;
     const float* r = rows.row(row);
     // sample: the whole row if it fits, else P pieces of 256 contiguous elements spread evenly
     int S;
@@ -320,8 +295,6 @@ __global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int6
     if (few && threadIdx.x < CS_SH) ws.shcnt[(row * CS_SH + threadIdx.x) * RCS] = 0;
     if (few)                                              // the row's global histogram of k_cs_pass
         for (int i = threadIdx.x; i < HBINS; i += NT) ws.hist[row * HBINS + i] = 0;
-    if (lone)                                             // the lone row's (k_lone_finish path)
-        for (int i = threadIdx.x; i < HBINS; i += NT) ws.lhist[(size_t)i * ws.lh_stride] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -858,11 +831,8 @@ template <int RING, int FGS, int LONE = 0>
 #ifndef FLC_TK_WPE
 #define FLC_TK_WPE 1                 // unconstrained (143 VGPRs); 4 waves per SIMD spilled and ran slower
 #endif
-// LONE (a lone compressVector row): 1 — every float4 read is also written as zeros to zout, the
-// dense output the selected entries are then scattered into (no separate fill of the output);
-// 2 — the k_lone_finish path: the zeros are written beside the sample, and every staged entry adds
-// one to the row's first-digit histogram (k_cs_pass's first digit, memory-side atomics at the
-// group's copy-out), so the one launch after the filter can pick the digit itself.
+// LONE (a lone compressVector row on the list path): every float4 read is also written as zeros to
+// zout, the dense output the selected entries are then scattered into (no separate fill of the output).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE))) void k_topk_filter_fast(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t rb, int64_t d, SelWs ws, int shards,
                                                                                                 float* __restrict__ zout) {
     static_assert(16 % RING == 0, "ring must divide the 16 loads of a chunk");
@@ -971,25 +941,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
             }
         }
 #endif
-        if constexpr ((LONE & 2) != 0) {
-            // first digit of dk = key - T over the row's histogram (k_cs_pass's, same shift)
-            if (fits && ptot) {
-                const uint32_t Tr = sload(ws.thr + prow), span = sload(ws.prefix + prow) - Tr;
-                uint32_t s0 = 0;
-                while (s0 < 21 && (((uint64_t)span * 4u) >> s0) >= (uint64_t)HBINS) ++s0;
-                uint32_t* gh = ws.lhist;                                 // lone row: prow == 0
-                const uint32_t hs = ws.lh_stride;
-                const float* svf = reinterpret_cast<const float*>(st[pb][wv] + SROW);
-                // not the clamp bin (HBINS - 1: every key past the first digit's range, the row's largest
-                // — ~10-20 K entries on one address, whose atomics serialise: 0.35 ms a call measured);
-                // k_lone_finish takes its count as the list's total minus the other bins
-                for (uint32_t e = (uint32_t)lane; e < ptot; e += 64) {
-                    const uint32_t dg = (mag_key(svf[e]) - Tr) >> s0;
-                    if (dg < (uint32_t)(HBINS - 1))
-                        __hip_atomic_fetch_add(gh + (size_t)dg * hs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-        }
     };
     while (it < items) {
         // key >= max(T, 1): the loads past the row end return +0 (key 0), so no per-element range
@@ -1021,7 +972,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
             }
             const uint32_t cnt0 = cnt;
             __amdgpu_buffer_rsrc_t ro;
-            if constexpr ((LONE & 1) != 0) ro = chunk_rsrc(zout, j0, d);
+            if constexpr (LONE != 0) ro = chunk_rsrc(zout, j0, d);
             // opaque per-chunk copy of the lane offset: stops LICM from hoisting the 64 per-(load,
             // component) index constants out of the loop into 64 live VGPRs
             uint32_t lb = (uint32_t)j0 + (uint32_t)lane * 4u;   // row index of the lane's element 0
@@ -1031,7 +982,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 const int P = L + RING - 1;
                 ring[P % RING] = P < 16 ? load_q(rs, lane, P) : load_q(rsn, lane, P - 16);
                 const float4 x = ring[L % RING];
-                if constexpr ((LONE & 1) != 0) {
+                if constexpr (LONE != 0) {
                     // unconditional (range-checked): one more store per step in the vmcnt queue
                     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
                     const u4v z = {0u, 0u, 0u, 0u};
@@ -2366,140 +2317,6 @@ __global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d,
     }
 }
 
-// A lone compressVector row, the short path: after k_topk_sample wrote the output's zeros and
-// k_topk_filter_fast<LONE = 2> left the row's first-digit histogram, the digit, the ranking of its bin
-// and the scatter in ONE launch (instead of k_cs_pass x 2 + k_assign_finish).  Every workgroup reads
-// the histogram and picks the first digit itself (hist_find: k_cs_pass's first pass, same bin), then
-// walks its shard of the list: entries above the digit's bin are in the top K whatever the rest
-// (their keys exceed every key of the bin, which holds the K-th) and are scattered at once; entries
-// in the bin go to the row's bin list (k_cs_pass list mode).  The last workgroup to arrive ranks the
-// bin's entries by (key desc, tie order) — the K-th key and the tie cut at once — and scatters the
-// admitted ones.  A row the digit does not settle (overflow, short list, K-th key in the clamp bin,
-// a bin over CS_LCAP entries, a count mismatch) takes exact_row in one workgroup, which scatters its
-// rewritten list (any entry scattered before is in it, with the same value).  Row state as k_cs_pass
-// leaves it (thr, krem, tiecut, flags: flc_select_row_flags).
-template <bool VEC>
-__global__ __launch_bounds__(EX_NT) void k_lone_finish(RowSrc rows, int64_t d, int64_t K, SelWs ws, float* __restrict__ out) {
-    __shared__ uint32_t h[HBINS];
-    __shared__ uint32_t scratch[260];
-    __shared__ uint32_t wsum[EX_NT / 64];
-    __shared__ uint64_t lst[CS_LCAP];
-    __shared__ uint64_t kth_s;
-    __shared__ uint32_t last_wg;
-    const uint32_t b = blockIdx.x, B = gridDim.x;                        // B == CS_SH: shard b
-    uint32_t cnt = 0;
-    for (int k = 0; k < CS_SH; ++k) cnt += ws.shcnt[k * RCS];
-    const uint32_t T = ws.thr[0], span = ws.prefix[0] - T;              // kest >= T
-    uint32_t s0 = 0;
-    while (s0 < 21 && (((uint64_t)span * 4u) >> s0) >= (uint64_t)HBINS) ++s0;
-    auto exact = [&]() {
-        if (threadIdx.x == 0 && ws.flags[0] == 0u) ws.flags[0] = F_SHORT;
-        exact_row<VEC>(rows, 1, 0, d, K, ws, h, scratch, wsum);
-        __threadfence_block();
-        const uint32_t c = ws.rowcnt[0];
-        for (uint32_t e = threadIdx.x; e < c; e += EX_NT) out[ws.ent_idx[e]] = ws.ent_val[e];
-    };
-    // read once per workgroup (workgroup 0 may set flags below while others read them): a workgroup
-    // seeing flags set by workgroup 0's exact path returns as it does, so the outcome is the same
-    if (threadIdx.x == 0) last_wg = (ws.flags[0] != 0u || cnt < (uint32_t)K) ? 1u : 0u;
-    __syncthreads();
-    bool fail = last_wg != 0u;
-    __syncthreads();
-    uint32_t bin = 0, above = 0, last = 0;
-    if (!fail) {
-        if (threadIdx.x == 0) scratch[259] = 0;
-        __syncthreads();
-        uint32_t part = 0;
-        for (int t = threadIdx.x; t < HBINS - 1; t += EX_NT) { const uint32_t v = ws.lhist[(size_t)t * ws.lh_stride]; h[t] = v; part += v; }
-        part = wave_sum(part);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&scratch[259], part);
-        __syncthreads();
-        if (threadIdx.x == 0) h[HBINS - 1] = cnt - scratch[259];          // the clamp bin: not counted by the filter
-        __syncthreads();
-        hist_find(h, (uint32_t)K, bin, above, scratch);
-        last = h[bin];
-        fail = bin == HBINS - 1 || last > (uint32_t)CS_LCAP;
-    }
-    if (fail) {
-        if (b == 0) exact();
-        return;
-    }
-    const uint32_t krem = (uint32_t)K - above;                           // >= 1: the K-th is in the bin
-    const int64_t segcap = (ws.cap / CS_SH) & ~int64_t(3);
-    const uint32_t mycnt = ws.shcnt[b * RCS];
-    const float* sv = ws.ent_val + b * segcap;
-    const uint32_t* si = ws.ent_idx + b * segcap;
-    if (threadIdx.x == 0) scratch[0] = 0;
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < mycnt; e += EX_NT) {
-        const float v = sv[e];
-        const uint32_t ix = si[e], key = mag_key(v);
-        const uint32_t dg = min((key - T) >> s0, (uint32_t)(HBINS - 1));
-        if (dg > bin) {
-            out[ix] = v;
-        } else if (dg == bin) {
-            const uint32_t slot = atomicAdd(&scratch[0], 1u);
-            if (slot < (uint32_t)CS_LCAP) lst[slot] = ((uint64_t)key << 32) | (uint64_t)tie_pref(ix, ws.tie_hi);
-        }
-    }
-    __syncthreads();
-    const uint32_t nl = min(scratch[0], (uint32_t)CS_LCAP);
-    if (threadIdx.x == 0) scratch[1] = nl ? atomicAdd(&ws.cstate[5], nl) : 0u;
-    __syncthreads();
-    uint64_t* gl = ws.clist;
-    const uint32_t gb = scratch[1];
-    for (uint32_t i = threadIdx.x; i < nl; i += EX_NT)
-        if (gb + i < (uint32_t)CS_LCAP) gl[gb + i] = lst[i];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                     // list and scatter stores done
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        last_wg = atomicAdd(&ws.carrive[0], 1u) == B - 1u ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!last_wg) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (threadIdx.x == 0) atomicExch(&ws.carrive[0], 0u);
-    const uint32_t m = __hip_atomic_load(&ws.cstate[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(m == last && m >= krem)) {                                     // every entry of the bin arrived
-        exact();
-        return;
-    }
-    for (uint32_t i = threadIdx.x; i < m; i += EX_NT)
-        lst[i] = __hip_atomic_load(&gl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) { scratch[2] = 0; scratch[3] = 0; }
-    __syncthreads();
-    // the entry of rank krem - 1 is the K-th: its key the threshold, its index the tie cut
-    for (uint32_t i = threadIdx.x; i < m; i += EX_NT) {
-        const uint64_t me = lst[i];
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < m; ++j) rank += lst[j] > me ? 1u : 0u;
-        if (rank == krem - 1u) kth_s = me;                               // entries are distinct
-    }
-    __syncthreads();
-    const uint64_t kc = kth_s;
-    const uint32_t kth = (uint32_t)(kc >> 32);
-    const float* r = rows.row(0);
-    for (uint32_t i = threadIdx.x; i < m; i += EX_NT) {
-        const uint64_t me = lst[i];
-        const uint32_t key = (uint32_t)(me >> 32);
-        if (me >= kc) {
-            const uint32_t ix = tie_pref((uint32_t)me, ws.tie_hi);      // tie_pref is its own inverse
-            out[ix] = r[ix];
-        }
-        if (key > kth) atomicAdd(&scratch[2], 1u);
-        else if (key == kth) atomicAdd(&scratch[3], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t gt = scratch[2], eq = scratch[3];
-        ws.thr[0] = kth;
-        ws.krem[0] = krem - gt;                                          // ties admitted
-        if (gt + eq > krem) { ws.tiecut[0] = tie_pref((uint32_t)kc, ws.tie_hi); ws.flags[0] |= F_TIES; }
-    }
-}
-
-
 // ------------------------------------------------------------------------------------------
 // A lone compressVector row held in the chip's registers: the exact selection in ONE launch.
 // The row (up to RS_U float4 a thread x 1024 threads x one workgroup per CU: 16.7 M elements on 256
@@ -3057,7 +2874,6 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
     const int64_t C = std::max<int64_t>(host_chunks(d), 1), nn = std::max<int64_t>(n, 1);
     SelWs s;
     s.tie_hi = 0;
-    s.lh_stride = 1;
     s.cap = sel_capacity(codec, d, K);
     s.tab = cv.take<uint2>((size_t)C * nn);
     s.ent_idx = cv.take<uint32_t>((size_t)nn * s.cap);
@@ -3075,7 +2891,6 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tieprefix = cv.take<uint32_t>((size_t)C * nn);
         s.tiecut = cv.take<uint32_t>(nn);
         s.hist = cv.take<uint32_t>((size_t)nn * HBINS);
-        s.lhist = cv.take<uint32_t>((size_t)HBINS * FLC_LONE_HSMAX);
         s.cursor = nullptr;
         s.cstate = cv.take<uint32_t>((size_t)nn * CS_ST);
         s.clist = cv.take<uint64_t>((size_t)std::min<int64_t>(nn, CS_FEW) * CS_LCAP);
@@ -3085,7 +2900,6 @@ static SelWs carve_sel(void* base, int codec, int64_t n, int64_t d, int64_t K, s
         s.tieprefix = nullptr;
         s.tiecut = nullptr;
         s.hist = nullptr;
-        s.lhist = nullptr;
         s.cursor = cv.take<uint32_t>((size_t)std::max<int64_t>(C, RK_SB) * nn);   // RandK: [N][RK_SB] segment offsets
         s.cstate = nullptr;
         s.clist = nullptr;
@@ -3133,7 +2947,7 @@ static bool cs_single() {            // tuning runs: FLC_CS_SINGLE=1 keeps the o
 
 #ifndef FLC_LONE_PATH
 #define FLC_LONE_PATH 2                // a lone compressVector row: 2 in registers (k_lone_resident, rows up to
-#endif                                 // RS_U * 4096 per CU; longer: 0), 1 three launches (k_lone_finish), 0 five
+#endif                                 // RS_U * 4096 per CU; longer: the list path), 0 the list path
 #ifndef FLC_RS_COOP
 #define FLC_RS_COOP 0                  // 1: k_lone_resident launched cooperatively (HIP's launch: +22 us a call
 #endif                                 // measured; residency holds anyway: G <= CUs, one workgroup per CU, launches serialised)
@@ -3165,18 +2979,6 @@ static int lone_path() {           // tuning runs: env FLC_LONE_PATH overrides
     return v;
 }
 
-static bool lone_zs() {           // the short path's output zeros beside the sample (1) or in the filter (0)
-    static const bool v = [] { const char* e = tuning_env("FLC_LONE_ZS"); return e ? atoi(e) != 0 : true; }();
-    return v;
-}
-static uint32_t lone_hs() {
-    static const uint32_t v = [] {
-        const char* e = tuning_env("FLC_LONE_HS");
-        return (uint32_t)std::min<int64_t>(std::max<int64_t>(e ? atoll(e) : FLC_LONE_HS, 1), FLC_LONE_HSMAX);
-    }();
-    return v;
-}
-
 static int filter_group() {
     static const int g = [] {
         const char* e = tuning_env("FLC_FILTER_GS");     // tuning runs only
@@ -3187,7 +2989,7 @@ static int filter_group() {
 
 template <int FGS>
 static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_t d, SelWs ws, hipStream_t st,
-                          int shards, float* zout = nullptr, int lone = 0) {
+                          int shards, float* zout = nullptr) {
     // oversubscribed grid (measured: 16-32 K blocks beat a resident-only persistent grid by ~5 %,
     // the hardware dispatcher balances the tail)
     const int64_t waves = rn * ((nchunks(d) + FGS - 1) / FGS);
@@ -3198,13 +3000,7 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)64;
     }();
     ProfScope _pv(FGS == 4 ? "k_topk_filter_g4" : "k_topk_filter_g2", st);   // which variant ran (tests)
-    if (lone == 2)
-        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, 2>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
-                           std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
-    else if (lone == 3)
-        hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, 3>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
-                           std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
-    else if (zout)
+    if (zout)
         hipLaunchKernelGGL((k_topk_filter_fast<FLC_TK_RING, FGS, 1>), dim3(gw), dim3(256), 0, st, rows, n, r0, rn,
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, zout);
     else
@@ -3410,10 +3206,9 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
     if (codec == FLC_TOPK) {
         if (prm->tie != FLC_TIE_LOWEST && prm->tie != FLC_TIE_HIGHEST) { set_error("topk: unknown tie rule %d", prm->tie); return FLC_ERR_ARG; }
         ws.tie_hi = prm->tie == FLC_TIE_HIGHEST ? 1u : 0u;
-        ws.lh_stride = lone_hs();
     }
     const int64_t C = host_chunks(d);
-    bool lone_assign = false, lone_short = false, gfold = false;
+    bool lone_assign = false, gfold = false;
     // TopK, few rows: sharded candidate lists (k_topk_filter_fast) and the spread select (k_cs_pass)
     const bool few = codec == FLC_TOPK && n <= CS_FEW && !cs_single() && sel_capacity(codec, d, K) >= (int64_t)CS_SH * GCAP;
     if (codec == FLC_RANDK) {
@@ -3481,9 +3276,6 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         // a lone compressVector (assign, one row) on the fast path: output zeros from the filter, the
         // exact fallback and the scatter in one launch (k_assign_finish)
         lone_assign = assign && n == 1 && few && !dense_k && !assign_fold();
-        // ... in three launches (k_lone_finish after the filter) unless a tuning run asks for the
-        // five-launch path (k_cs_pass x 2 + k_assign_finish)
-        lone_short = lone_assign && lone_path() == 1;
 
         if (dense_k) FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const int64_t bpr = (C + 3) / 4;
@@ -3491,10 +3283,8 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             { ProfScope _ps("k_topk_sample", st);
             // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3);
             // the short lone-row path: one more workgroup per 16 chunks writes the output's zeros
-            const bool zs = lone_short && lone_zs();
-            const unsigned zb = zs ? (unsigned)((C + 15) / 16) : 0u;
-            hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)n + zb), dim3(1024), 0, st, rows, n, d, K, ws,
-                               few ? 1 : 0, lone_short ? 1 : 0, zs ? out : (float*)nullptr); }
+            hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
+                               few ? 1 : 0); }
             FLC_CHECK_LAUNCH("k_topk_sample");
             // per row group: filter (the full read), then the candidate select and the exact
             // fallback of the group's rows; with TG > 1 groups the select + fallback of group g run
@@ -3529,11 +3319,9 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 // few rows: 2-chunk groups (twice the waves in flight for a lone row)
                 // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
                 // a lone compressVector row: the filter also writes the dense output's zeros
-                // (the short path: zeros here unless beside the sample, + the first-digit histogram)
-                float* zout = lone_assign && !(lone_short && lone_zs()) ? out : nullptr;
-                const int lone = lone_short ? (zout ? 3 : 2) : 0;
-                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout, lone);
-                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout, lone); }
+                float* zout = lone_assign ? out : nullptr;
+                if (filter_group() == 2 || n * d < ((int64_t)64 << 20)) launch_filter<2>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout);
+                else launch_filter<4>(rows, n, r0, rn, d, ws, st, few ? CS_SH : 1, zout); }
                 FLC_CHECK_LAUNCH("k_topk_filter");
                 if (TG > 1) {
                     FLC_CHECK_HIP(hipEventRecord(cx->ev[g], st));
@@ -3545,9 +3333,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 // settle a row whose first digit's bin holds <= CS_LCAP entries (~(4 sqrt(ks) + 8)
                 // D / 16 K spread over 256-512 bins: up to ~900 at D = 64 M), else 3 cover every
                 // shift; many rows: 512-thread workgroups (measured 0.289 -> 0.263 ms against 256 at C3)
-                if (lone_short) {
-                    // the digit, its bin's ranking and the scatter: k_lone_finish below
-                } else if (few) {
+                if (few) {
                     const int np = (FLC_CS_LIST && d <= FLC_CS_TWO_MAXD) ? 2 : 3;
                     for (int p = 0; p < np; ++p)
                         hipLaunchKernelGGL(k_cs_pass, dim3((unsigned)CS_SH, (unsigned)n), dim3(CS_NT), 0, st, K, ws,
@@ -3631,13 +3417,6 @@ if (vec) hipLaunchKernelGGL((k_topk_filter<true, true>), dim3(gb), dim3(256), 0,
     }
     // Every row's list now holds exactly its admitted entries plus, on the fast path, candidates
     // below the exact threshold; k_chunk_accum admits key >= thr.
-    if (lone_short) {
-        ProfScope _ps("k_lone_finish", st);
-        if (vec) hipLaunchKernelGGL((k_lone_finish<true>), dim3(CS_SH), dim3(EX_NT), 0, st, rows, d, K, ws, out);
-        else hipLaunchKernelGGL((k_lone_finish<false>), dim3(CS_SH), dim3(EX_NT), 0, st, rows, d, K, ws, out);
-        FLC_CHECK_LAUNCH("k_lone_finish");
-        return FLC_OK;
-    }
     if (lone_assign) {
         // output zeros written by the filter; exact fallback (if the row failed) + scatter
         ProfScope _ps("k_assign_finish", st);

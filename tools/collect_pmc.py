@@ -12,6 +12,7 @@ cdna_hip_programming.md §7).  Writes to profiles/pmc_<wl>.json, which bench.py 
 roofline.traffic.
 
 usage: python tools/collect_pmc.py --workload c3 [--n N] [--steps 2]
+       python tools/collect_pmc.py --dropin --workload c3 --n 8     (one compressVector: profiles/pmc_dropin_c3.json)
 """
 import argparse
 import collections
@@ -27,9 +28,12 @@ KERNEL_SUBSTR = {"c3": "k_topk_filter_fast", "c4": "k_ds_filter", "reduce": "k_r
                  "c2": "k_randk_gen", "c5": "k_ds_filter"}
 
 
+DROPIN_KERNEL = {"c3": "k_lone_resident", "c4": "k_lone_dither"}
+
+
 def run_pass(ctr, wl, extra, outdir, kernel):
     cmd = ["rocprofv3", "--pmc", ctr, "-d", outdir, "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--no-cpu-baseline"] + extra
+           sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl] + extra
     subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL, timeout=600)
     vals, disp = collections.defaultdict(float), set()
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
@@ -48,16 +52,18 @@ def main():
     ap.add_argument("--kernel", default=None, help="another kernel of the workload (default: its dominant one)")
     ap.add_argument("--tag", default=None, help="output name profiles/pmc_<tag>.json (default: the workload)")
     ap.add_argument("--compat", action="store_true", help="the compat-pattern line (resident numpy-stream patterns)")
+    ap.add_argument("--dropin", action="store_true", help="the drop-in line's compressVector kernel")
     a = ap.parse_args()
-    kernel = a.kernel or KERNEL_SUBSTR[a.workload]
-    tag = a.tag or (a.workload + ("_compat" if a.compat else ""))
+    kernel = a.kernel or (DROPIN_KERNEL if a.dropin else KERNEL_SUBSTR)[a.workload]
+    tag = a.tag or (("dropin_" if a.dropin else "") + a.workload + ("_compat" if a.compat else ""))
     extra = ["--steps", str(a.steps), "--warmup", "1"] + (["--n", str(a.n)] if a.n else []) + (["--compat"] if a.compat else [])
+    extra += ["--dropin"] if a.dropin else ["--no-cpu-baseline"]
     os.environ.setdefault("TMPDIR", "/tmp")
     base = os.path.join(ROOT, "gpurun_out", f"pmc_traffic_{tag}")
     fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch", kernel)
     write, nw = run_pass("WRITE_SIZE", a.workload, extra, base + "_write", kernel)
     launches = max(nf, nw, 1)
-    res = {"workload": a.workload, "kernel": kernel, "n_override": a.n, "compat": bool(a.compat),
+    res = {"workload": a.workload, "kernel": kernel, "n_override": a.n, "compat": bool(a.compat), "dropin": bool(a.dropin),
            "launches": launches, "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024 / launches),
            "correction": "2 x FETCH_SIZE (gfx950 tallies each 128-B line request at 64 B: every streamed "

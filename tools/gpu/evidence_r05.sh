@@ -15,6 +15,8 @@ for wl in c3 c4 c2; do
   timeout -k 10 400 python tools/collect_pmc.py --workload $wl > $out/pmc_$wl.log 2>&1 || exit $?
 done
 timeout -k 10 500 python tools/collect_pmc.py --workload c4 --compat --n 256 --steps 1 > $out/pmc_c4_compat.log 2>&1 || exit $?
+timeout -k 10 400 python tools/collect_pmc.py --dropin --workload c3 --n 8 --steps 5 > $out/pmc_dropin_c3.log 2>&1 || exit $?
+timeout -k 10 400 python tools/collect_pmc.py --dropin --workload c4 --n 4 --steps 5 > $out/pmc_dropin_c4.log 2>&1 || exit $?
 echo "pmc done"
 for wl in c3 c4 c2 c5; do
   st=20; wu=3; [ $wl = c5 ] && { st=5; wu=2; }
@@ -22,6 +24,8 @@ for wl in c3 c4 c2 c5; do
      python bench.py --workload $wl --steps $st --warmup $wu > $out/bench_$wl.log 2>&1 || exit $?
   echo "$wl: $(tail -1 $out/bench_$wl.log | cut -c1-200)"
 done
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/stats_dropin_c3 -o run --output-format csv -- \
+   python bench.py --dropin --workload c3 --n 8 --steps 10 --warmup 2 > $out/dropin_c3_prof.log 2>&1 || exit $?
 B="timeout -k 10 400 python bench.py"
 $B > $out/bench_default.log 2>&1 || exit $?
 $B --workload c4 --no-cpu-baseline > $out/bench_c4_plain.log 2>&1 || exit $?
