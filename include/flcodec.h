@@ -321,8 +321,10 @@ int flc_profile_collect(const char* kernel, double* h_total_ms, int64_t* h_launc
  * same params, n and d — into d_flags[n] (device, on `stream`).  Bits: 1 the candidate list
  * overflowed, 2 it came up short, 4 ambiguous ties at the K-th key resolved on the fast path,
  * 8 the row was selected by the exact path (the fast path failed — bits 1 / 2 then say why — or
- * K > D/16).  Rows that stayed on the fast path read 0 or 4.  (Replaces nothing in the reference: compressors.py:330-335 has
- * one path.) */
+ * K > D/16), 16 a lone compressVector row (flc_encode, n = 1) selected exactly in registers in one
+ * launch (rows up to 16 float4 x 4096 x the device's CUs; 4 then marks a tie cut, 1 a grid wait
+ * that gave up).  Rows that stayed on the fast path read 0 or 4.  (Replaces nothing in the
+ * reference: compressors.py:330-335 has one path.) */
 int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* d_workspace,
                          size_t ws_bytes, uint32_t* d_flags, void* stream);
 
