@@ -35,6 +35,12 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Layout / probe switches for A/B tuning runs.  Only a build with -DFLC_TUNING (tools/ab_build.sh
 // --tuning) reads them from the environment; the product library ignores the environment, so a
 // stray variable can never change a result.
+// Events that only order one device's streams (hipStreamWaitEvent; never inspected by the host):
+// device-scope release, no system-scope cache writeback at each record
+#ifndef FLC_SYNC_EVENT_FLAGS
+#define FLC_SYNC_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+
 inline const char* tuning_env(const char* name) {
 #ifdef FLC_TUNING
     return getenv(name);

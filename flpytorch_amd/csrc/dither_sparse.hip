@@ -1809,7 +1809,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
     }
     while ((int)cx.ev.size() < std::max(K, TO) + 2) {
         hipEvent_t e;
-        FLC_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        FLC_CHECK_HIP(hipEventCreateWithFlags(&e, FLC_SYNC_EVENT_FLAGS));
         cx.ev.push_back(e);
     }
     if (K == 1) {

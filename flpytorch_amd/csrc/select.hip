@@ -2674,29 +2674,53 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             pos += scratch[0];
         }
         uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
+        // the listed elements first: their stores are done at the arrival (rs_arrive waits for
+        // them); the dense output is stored after it, without the listed positions (the last
+        // workgroup writes those), so its 8 D bytes drain under the ranking instead of before it
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             if (u < uv) {
                 const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                uint32_t o[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const uint32_t kp = mag_key(e[q]) >> 9;
                     const uint32_t j = (f0 + u * RS_NT) * 4u + (uint32_t)q;
-                    o[q] = kp > P ? __float_as_uint(e[q]) : 0u;
-                    if (kp == P && (int64_t)j < d) {
+                    if ((mag_key(e[q]) >> 9) == P && (int64_t)j < d) {
                         if (pos < (uint32_t)RS_CAP)
                             __hip_atomic_store(cl + pos, ((uint64_t)__float_as_uint(e[q]) << 32) | j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         ++pos;
                     }
                 }
-                const u4v ov = {o[0], o[1], o[2], o[3]};
-                __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, 0);
             }
         }
+        auto dense = [&]() {
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                if (u < uv) {
+                    const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                    uint32_t o[4];
+                    bool at[4], any = false;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t kp = mag_key(e[q]) >> 9;
+                        o[q] = kp > P ? __float_as_uint(e[q]) : 0u;
+                        at[q] = kp == P;
+                        any |= at[q];
+                    }
+                    if (!any) {
+                        const u4v ov = {o[0], o[1], o[2], o[3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, 0);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (!at[q]) __builtin_amdgcn_raw_buffer_store_b32(o[q], ro, voff + 4u * q, u * RS_NT * 16, 0);
+                    }
+                }
+            }
+        };
         RS_STAMP(10);
         if (rs_arrive(tr, &flag_s, &gen_s, 0u)) {
-            // the last workgroup: rank the m listed elements, keep the krem first
+            // the last workgroup: rank the m listed elements, store the krem first and +0 for the
+            // rest (then its own dense output)
             __shared__ uint64_t comp[RS_CAP];
             __shared__ uint64_t kth_s;
             const uint32_t m = __hip_atomic_load(ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2718,17 +2742,14 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             __syncthreads();
             const uint64_t kc = kth_s;
             const uint32_t kth = (uint32_t)(kc >> 32);
-            if (ok)
-                for (uint32_t i = t; i < mm; i += RS_NT) {
-                    const uint64_t me = comp[i];
-                    if (me >= kc) {
-                        const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        out[(uint32_t)en] = __uint_as_float((uint32_t)(en >> 32));
-                    }
-                    const uint32_t key = (uint32_t)(me >> 32);
-                    if (key > kth) atomicAdd(&scratch[2], 1u);
-                    else if (key == kth) atomicAdd(&scratch[3], 1u);
-                }
+            for (uint32_t i = t; i < mm; i += RS_NT) {
+                const uint64_t me = comp[i];
+                const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                out[(uint32_t)en] = (ok && me >= kc) ? __uint_as_float((uint32_t)(en >> 32)) : 0.f;
+                const uint32_t key = (uint32_t)(me >> 32);
+                if (key > kth) atomicAdd(&scratch[2], 1u);
+                else if (key == kth) atomicAdd(&scratch[3], 1u);
+            }
             __syncthreads();
             if (t == 0) {
                 __hip_atomic_store(ctl + RS_CCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // clean for the next call
@@ -2739,6 +2760,9 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 ws.tiecut[0] = tie_pref((uint32_t)kc, ws.tie_hi);
                 ws.flags[0] = F_RESIDENT | (gt + eq > krem ? F_TIES : 0u) | ((gave_up || !ok) ? F_OVERFLOW : 0u);
             }
+            dense();
+        } else {
+            dense();
         }
         RS_STAMP(11);
     } else {
@@ -2948,6 +2972,9 @@ static bool cs_single() {            // tuning runs: FLC_CS_SINGLE=1 keeps the o
 #ifndef FLC_LONE_PATH
 #define FLC_LONE_PATH 2                // a lone compressVector row: 2 in registers (k_lone_resident, rows up to
 #endif                                 // RS_U * 4096 per CU; longer: the list path), 0 the list path
+#ifndef FLC_RS_EVREC
+#define FLC_RS_EVREC 1                 // the completion event recorded after every resident launch (0: at a stream switch)
+#endif
 #ifndef FLC_RS_COOP
 #define FLC_RS_COOP 0                  // 1: k_lone_resident launched cooperatively (HIP's launch: +22 us a call
 #endif                                 // measured; residency holds anyway: G <= CUs, one workgroup per CU, launches serialised)
@@ -3244,11 +3271,14 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 if (!rc.ctl) {
                     FLC_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&rc.ctl), (size_t)RS_CTL * sizeof(uint32_t)));
                     FLC_CHECK_HIP(hipMemset(rc.ctl, 0, (size_t)RS_CTL * sizeof(uint32_t)));
-                    FLC_CHECK_HIP(hipEventCreateWithFlags(&rc.done, hipEventDisableTiming));
+                    FLC_CHECK_HIP(hipEventCreateWithFlags(&rc.done, FLC_SYNC_EVENT_FLAGS));
                 }
                 hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
                 FLC_CHECK_HIP(hipStreamIsCapturing(st, &cap));
-                if (rc.last && rc.last != st && cap == hipStreamCaptureStatusNone) FLC_CHECK_HIP(hipStreamWaitEvent(st, rc.done, 0));
+                if (rc.last && rc.last != st && cap == hipStreamCaptureStatusNone) {
+                    if (!FLC_RS_EVREC) FLC_CHECK_HIP(hipEventRecord(rc.done, rc.last));   // (probe builds)
+                    FLC_CHECK_HIP(hipStreamWaitEvent(st, rc.done, 0));
+                }
                 const int e4i = (int)e4;
                 if (FLC_RS_COOP) {
                     RowSrc ra = rows;
@@ -3265,7 +3295,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                     hipLaunchKernelGGL((k_lone_resident<RS_U>), dim3((unsigned)Gu), dim3(RS_NT), 0, st, rows, d, K, ws, out, e4i, rc.ctl, ++rc.seq);
                 }
                 if (cap == hipStreamCaptureStatusNone) {
-                    FLC_CHECK_HIP(hipEventRecord(rc.done, st));
+                    if (FLC_RS_EVREC) FLC_CHECK_HIP(hipEventRecord(rc.done, st));
                     rc.last = st;
                 }
                 FLC_CHECK_LAUNCH("k_lone_resident");
@@ -3308,7 +3338,7 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 }
                 while ((int)cx->ev.size() < TG + 1) {
                     hipEvent_t e;
-                    FLC_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    FLC_CHECK_HIP(hipEventCreateWithFlags(&e, FLC_SYNC_EVENT_FLAGS));
                     cx->ev.push_back(e);
                 }
                 sside = cx->side;
