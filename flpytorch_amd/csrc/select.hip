@@ -53,14 +53,17 @@ constexpr int RS_U = 16;             // (<= 16: kept-tie mask of 64 bits) k_lone
 #define FLC_RS_NG 4                   // k_lone_resident: workgroup groups (histogram replicas, barrier tree);
 #endif                                // us a call at D = 10 M: 1 -> 57, 2 -> 53, 4 -> 52, 8 -> 54.6, 16 -> 60
 constexpr int RS_NG = FLC_RS_NG;
+constexpr int RS_NG_MAX = 16;
+static_assert(RS_NG >= 1 && RS_NG <= RS_NG_MAX, "FLC_RS_NG: 1..16 groups");
 // its control words: counters on lines of their own, per-group digit histograms, tie counts
 constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128;
+constexpr int RS_ABV = RS_GRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
 constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
 #ifndef FLC_RS_SPEC
 #define FLC_RS_SPEC 1                 // k_lone_resident: speculative first digit (two digits in one round)
 #endif
-constexpr int RS_HREP = RS_GRP + 32 * RS_NG;
+constexpr int RS_HREP = RS_ABV + 32 * RS_NG_MAX;
 constexpr int RS_HSPEC = RS_HREP + 3 * RS_NG * HBINS;    // [RS_NG][3][HBINS] speculative second digit
 constexpr int RS_CLIST = RS_HSPEC + 3 * RS_NG * HBINS;   // [RS_CAP] (value bits, index)
 constexpr int RS_TCNT = RS_CLIST + 2 * RS_CAP;
@@ -2459,14 +2462,16 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     // (32 spread pieces of 256), the same in every workgroup, loaded BEFORE the row so that it lands
     // first (vmcnt retires in order) and its digit is picked while the row streams in
     const bool spec = FLC_RS_SPEC && d >= 4 * (int64_t)RS_SS;
-    float4 sq0 = make_float4(0.f, 0.f, 0.f, 0.f), sq1 = sq0;
-    if (spec) {
-        const int64_t pos = (int64_t)(t >> 5) * (d - 256) / 31 + (int64_t)(t & 31) * 8;
-        const auto a = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)(pos * 4), 0, 0);
-        const auto b = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)(pos * 4 + 16), 0, 0);
-        sq0 = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
-        sq1 = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
-    }
+    // the release word's generation for the first round, loaded before everything else (by every
+    // thread, unconditionally): its wait then does not drain the row's loads (vmcnt is in order)
+    // (raw: the generation is masked out where it is used, so nothing waits for this load early)
+    const uint64_t gen_word = __hip_atomic_load(reinterpret_cast<const uint64_t*>(ctl + RS_GEN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the sample's loads unconditionally (an empty descriptor when there is no speculation: zeros,
+    // no memory access), so that no branch makes the compiler wait for them before the row's loads
+    const int64_t spos = spec ? (int64_t)(t >> 5) * (d - 256) / 31 + (int64_t)(t & 31) * 8 : 0;
+    const auto rsm = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(0)), (short)0, spec ? (int)nb : 0, 0x00020000);
+    const auto sa = __builtin_amdgcn_raw_buffer_load_b128(rsm, (uint32_t)(spos * 4), 0, 0);
+    const auto sb = __builtin_amdgcn_raw_buffer_load_b128(rsm, (uint32_t)(spos * 4 + 16), 0, 0);
     // the workgroup's part through a descriptor of its own extent: the loads past it (u >= e4, the
     // row end) return zeros without touching memory, so all RU are issued unconditionally and the
     // compiler's in-order vmcnt count stays exact (the sample's wait does not drain the row)
@@ -2486,24 +2491,29 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     if (spec) {
         __shared__ uint32_t h1[3 * HBINS];
-        const uint32_t gen = t == 0 ? rs_gen(tr) : 0u;
+        const uint32_t gen = (uint32_t)gen_word & 7u;
         for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
         for (int i = t; i < 3 * HBINS; i += RS_NT) h1[i] = 0;
         __syncthreads();
         {
-            const float e[8] = {sq0.x, sq0.y, sq0.z, sq0.w, sq1.x, sq1.y, sq1.z, sq1.w};
 #pragma unroll
-            for (int q = 0; q < 8; ++q) atomicAdd(&h[mag_key(e[q]) >> 20], 1u);
+            for (int q = 0; q < 4; ++q) {
+                atomicAdd(&h[(sa[q] & 0x7FFFFFFFu) >> 20], 1u);
+                atomicAdd(&h[(sb[q] & 0x7FFFFFFFu) >> 20], 1u);
+            }
         }
         __syncthreads();
         uint32_t ab;
         const uint32_t rs = (uint32_t)min((int64_t)RS_SS, max((int64_t)1, (K * RS_SS + d / 2) / d));
         hist_find(h, rs, bs, ab, scratch);                               // the sample's digit (uniform)
-        for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
         __syncthreads();
-        // the first digit's histogram, and the second digit's for the first digits bs - 1 .. bs + 1
+        // the second digit's histograms for the first digits bs - 1 .. bs + 1, and the count of keys
+        // whose first digit is above them: with the K-th key's first digit among the three, that is
+        // all the merger needs for both digits (the contended first-digit histogram — the exponents
+        // crowd into few bins — is not built at all unless the guess misses)
         uint32_t km = 0x7FFFFFFFu;
         asm volatile("" : "+s"(km));
+        uint32_t abv = 0;
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             if (u < uv) {
@@ -2511,63 +2521,82 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t k = __float_as_uint(e[q]) & km;
-                    const uint32_t b0 = k >> 20, w = b0 - bs + 1u;
-                    atomicAdd(&h[b0], 1u);
+                    const uint32_t w = (k >> 20) - bs + 1u;
                     if (w < 3u) atomicAdd(&h1[w * HBINS + ((k >> 9) & 0x7FFu)], 1u);
+                    else abv += (k >> 20) > bs + 1u ? 1u : 0u;
                 }
             }
         }
+        abv = wave_sum(abv);
+        if (t == 0) scratch[0] = 0;
+        __syncthreads();
+        if ((t & 63) == 0 && abv) atomicAdd(&scratch[0], abv);
         __syncthreads();
         RS_STAMP(1);
-        uint32_t* gh = ctl + RS_HREP + tr.grp * HBINS;
         uint32_t* gs = ctl + RS_HSPEC + tr.grp * 3 * HBINS;
-        for (int i = t; i < HBINS; i += RS_NT)
-            if (h[i]) __hip_atomic_fetch_add(gh + i, h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int i = t; i < 3 * HBINS; i += RS_NT)
             if (h1[i]) __hip_atomic_fetch_add(gs + i, h1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 && scratch[0]) __hip_atomic_fetch_add(ctl + RS_ABV + 32 * tr.grp, scratch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++bar;
         if (rs_arrive(tr, &flag_s, &gen_s, gen)) {
-            // the merger: the first digit exact; if it is among the three speculated, the second
-            // from the speculative replicas — both digits in ONE round (else the next round takes it)
+            // the merger: the three second-digit histograms summed (all loads in flight at once) with
+            // their totals; the first digit is the one of the three where the count from the top
+            // reaches K (else the guess missed: the rounds start from the first digit), the second
+            // from its histogram — both digits in ONE round
             RS_STAMP(2);
-            uint32_t* r0 = ctl + RS_HREP;
             uint32_t* s0 = ctl + RS_HSPEC;
-            for (int i = t; i < HBINS; i += RS_NT) {
-                uint32_t c = 0;
-#pragma unroll
-                for (int r = 0; r < RS_NG; ++r) c += __hip_atomic_load(r0 + r * HBINS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                h[i] = i == 0 ? c - pad : c;
-            }
+            if (t < 4) scratch[4 + t] = 0;
             __syncthreads();
-            uint32_t b0, a0;
-            hist_find(h, (uint32_t)K, b0, a0, scratch);
-            const uint32_t l0 = h[b0], w0 = b0 - bs + 1u;
-            uint64_t pl;
-            if (w0 < 3u) {                                               // (uniform) hit
-                for (int i = t; i < HBINS; i += RS_NT) {
+            uint32_t cw[3] = {0u, 0u, 0u};
+            for (int i = t; i < HBINS; i += RS_NT) {
+#pragma unroll
+                for (int w = 0; w < 3; ++w) {
                     uint32_t c = 0;
+                    const uint32_t* sw = s0 + w * HBINS + i;
 #pragma unroll
                     for (int r = 0; r < RS_NG; ++r)
-                        c += __hip_atomic_load(s0 + (r * 3 + w0) * HBINS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    h[i] = (i == 0 && b0 == 0u) ? c - pad : c;
+                        c += __hip_atomic_load(sw + r * 3 * HBINS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (i == 0 && bs + (uint32_t)w == 1u) c -= pad;         // the padding: first digit 0, second 0
+                    h1[w * HBINS + i] = c;
+                    cw[w] += c;
                 }
-                __syncthreads();
+            }
+            uint32_t A = 0;
+            if (t == 0)
+#pragma unroll
+                for (int r = 0; r < RS_NG; ++r) A += __hip_atomic_load(ctl + RS_ABV + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int w = 0; w < 3; ++w) {
+                const uint32_t c = wave_sum(cw[w]);
+                if ((t & 63) == 0 && c) atomicAdd(&scratch[4 + w], c);
+            }
+            if (t == 0) scratch[7] = A;
+            __syncthreads();
+            A = scratch[7];
+            const uint32_t c0 = scratch[4], c1 = scratch[5], c2 = scratch[6];
+            __syncthreads();
+            // windows from the top: bs + 1 (w 2), bs (w 1), bs - 1 (w 0)
+            int w0 = -1;
+            uint32_t a0 = A;
+            if (A < (uint32_t)K) {
+                if (A + c2 >= (uint32_t)K) w0 = 2;
+                else if (A + c2 + c1 >= (uint32_t)K) { w0 = 1; a0 = A + c2; }
+                else if (A + c2 + c1 + c0 >= (uint32_t)K) { w0 = 0; a0 = A + c2 + c1; }
+            }
+            uint64_t pl = 0;                                             // miss: start from the first digit
+            if (w0 >= 0) {                                               // (uniform)
                 uint32_t b1, a1;
-                hist_find(h, (uint32_t)K - a0, b1, a1, scratch);
+                hist_find(h1 + w0 * HBINS, (uint32_t)K - a0, b1, a1, scratch);
+                const uint32_t b0 = bs - 1u + (uint32_t)w0;
                 // hit | 22-bit prefix << 1 | krem << 23 | the prefix's count (saturated) << 47
                 pl = 1ull | ((uint64_t)((b0 << 11) | b1) << 1) | ((uint64_t)((uint32_t)K - a0 - a1) << 23) |
-                     ((uint64_t)min(h[b1], 16383u) << 47);
-            } else {
-                pl = ((uint64_t)b0 << 1) | ((uint64_t)((uint32_t)K - a0) << 23) | ((uint64_t)min(l0, 16383u) << 47);
+                     ((uint64_t)min(h1[w0 * HBINS + b1], 16383u) << 47);
             }
             rs_release(tr, &gen_s, pl);
             if (t == 0) { scratch[0] = (uint32_t)pl; scratch[1] = (uint32_t)(pl >> 32); }
-            for (int i = t; i < HBINS; i += RS_NT) {                     // clean for the next call
-#pragma unroll
-                for (int r = 0; r < RS_NG; ++r) __hip_atomic_store(r0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (int r = 0; r < 3 * RS_NG; ++r) __hip_atomic_store(s0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (t < RS_NG) __hip_atomic_store(ctl + RS_ABV + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int i = t; i < 3 * RS_NG * HBINS; i += RS_NT)           // clean for the next call
+                __hip_atomic_store(s0 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             RS_STAMP(2);
             rs_wait(tr, &gen_s, scratch);
@@ -2575,15 +2604,17 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         __syncthreads();
         const uint64_t pl = ((uint64_t)scratch[1] << 32) | scratch[0];
         __syncthreads();
-        prefix = (uint32_t)(pl >> 1) & 0x3FFFFFu;
-        krem = (uint32_t)(pl >> 23) & 0xFFFFFFu;
-        last = (uint32_t)(pl >> 47);
-        p0 = (pl & 1u) ? 2 : 1;
-        cand = p0 == 2 && last <= (uint32_t)RS_CAP;
+        if (pl & 1u) {
+            prefix = (uint32_t)(pl >> 1) & 0x3FFFFFu;
+            krem = (uint32_t)(pl >> 23) & 0xFFFFFFu;
+            last = (uint32_t)(pl >> 47);
+            p0 = 2;
+            cand = last <= (uint32_t)RS_CAP;
+        }                                                                // (else p0 = 0: the full rounds)
         RS_STAMP(3);
     }
     for (int p = p0; p < 3 && !cand; ++p) {
-        const uint32_t gen = t == 0 ? rs_gen(tr) : 0u;                   // (in flight under the histogram)
+        const uint32_t gen = (p == 0 && !spec) ? ((uint32_t)gen_word & 7u) : (t == 0 ? rs_gen(tr) : 0u);
         for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
         __syncthreads();
         // an opaque copy of the key mask per pass: keeps the compiler from hoisting the 4 RU keys out
