@@ -60,6 +60,9 @@ constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128
 constexpr int RS_ABV = RS_GRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
 constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
+#ifndef FLC_RS_STPOL
+#define FLC_RS_STPOL 2                // the dense output's stores: nontemporal (2) or default (0)
+#endif
 #ifndef FLC_RS_SPEC
 #define FLC_RS_SPEC 1                 // k_lone_resident: speculative first digit (two digits in one round)
 #endif
@@ -2739,11 +2742,11 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                     }
                     if (!any) {
                         const u4v ov = {o[0], o[1], o[2], o[3]};
-                        __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, FLC_RS_STPOL);
                     } else {
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
-                            if (!at[q]) __builtin_amdgcn_raw_buffer_store_b32(o[q], ro, voff + 4u * q, u * RS_NT * 16, 0);
+                            if (!at[q]) __builtin_amdgcn_raw_buffer_store_b32(o[q], ro, voff + 4u * q, u * RS_NT * 16, FLC_RS_STPOL);
                     }
                 }
             }
@@ -2870,7 +2873,7 @@ store:
                 o[q] = keep ? __float_as_uint(e[q]) : 0u;
             }
             const u4v ov = {o[0], o[1], o[2], o[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff, u * RS_NT * 16, FLC_RS_STPOL);
         }
     }
     RS_STAMP(11);
