@@ -198,11 +198,12 @@ __device__ inline uint32_t key_bin(uint32_t key, int p) {
 // DUAL (few rows: latency-bound): the two rank searches share their passes over the sample; the
 // second histogram costs 8 KB of LDS, which would halve the workgroups per CU of a many-row launch.
 template <int NT, bool DUAL>
-__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few) {
+__global__ __launch_bounds__(NT) void k_topk_sample(RowSrc rows, int64_t n, int64_t d, int64_t K, SelWs ws, int few,
+                                                    int64_t r_off) {
     __shared__ uint32_t keys[SMAX];
     __shared__ uint32_t h[HBINS], h2[DUAL ? HBINS : 1];
     __shared__ uint32_t scratch[260], scratch2[DUAL ? 260 : 1];
-    const int64_t row = blockIdx.x;
+    const int64_t row = r_off + blockIdx.x;                               // (a launch may take a row range)
     if (row >= n) return;
     const float* r = rows.row(row);
     // sample: the whole row if it fits, else P pieces of 256 contiguous elements spread evenly
@@ -3069,6 +3070,9 @@ static void launch_filter(RowSrc rows, int64_t n, int64_t r0, int64_t rn, int64_
                            std::min(rb, std::max<int64_t>(rn, 1)), d, ws, shards, (float*)nullptr);
 }
 
+#ifndef FLC_TK_SPLIT_SAMPLE
+#define FLC_TK_SPLIT_SAMPLE 1         // TopK row groups: only group 0's sample before the first filter
+#endif
 #ifndef FLC_TK_LASTPCT
 #define FLC_TK_LASTPCT 100            // size of the last TopK row group in % of the others (its tail is exposed)
 #endif
@@ -3344,12 +3348,6 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
         if (dense_k) FLC_CHECK_HIP(hipMemsetAsync(ws.hist, 0, (size_t)n * HBINS * sizeof(uint32_t), st));
         const int64_t bpr = (C + 3) / 4;
         if (!dense_k) {
-            { ProfScope _ps("k_topk_sample", st);
-            // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3);
-            // the short lone-row path: one more workgroup per 16 chunks writes the output's zeros
-            hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)n), dim3(1024), 0, st, rows, n, d, K, ws,
-                               few ? 1 : 0); }
-            FLC_CHECK_LAUNCH("k_topk_sample");
             // per row group: filter (the full read), then the candidate select and the exact
             // fallback of the group's rows; with TG > 1 groups the select + fallback of group g run
             // on a side stream under the filter of group g + 1 (both per-row, other rows' lists)
@@ -3370,15 +3368,39 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                     FLC_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
                     FLC_CHECK_HIP(hipStreamCreateWithPriority(&cx->side, hipStreamNonBlocking, hi));
                 }
-                while ((int)cx->ev.size() < TG + 1) {
+                while ((int)cx->ev.size() < TG + 3) {
                     hipEvent_t e;
                     FLC_CHECK_HIP(hipEventCreateWithFlags(&e, FLC_SYNC_EVENT_FLAGS));
                     cx->ev.push_back(e);
                 }
                 sside = cx->side;
             }
+            // the sample: group 0's rows before its filter; with row groups the other rows' samples run
+            // on the side stream beside group 0's filter (after the work queued before this call), and
+            // group 1's filter waits for them — only group 0's share of the sample is exposed
+            const bool split = FLC_TK_SPLIT_SAMPLE && TG > 1;
+            const int64_t rs1 = split ? group_row(n, TG, 1, FLC_TK_LASTPCT) : n;
+            auto sample = [&](int64_t a, int64_t b, hipStream_t sx) {
+                if (b <= a) return;
+                ProfScope _ps("k_topk_sample", sx);
+                // 1024-thread workgroups for any row count (measured 0.098 -> 0.066 ms against 256 at C3)
+                hipLaunchKernelGGL((few ? k_topk_sample<1024, true> : k_topk_sample<1024, false>), dim3((unsigned)(b - a)), dim3(1024), 0, sx,
+                                   rows, n, d, K, ws, few ? 1 : 0, a);
+            };
+            if (split) {
+                FLC_CHECK_HIP(hipEventRecord(cx->ev[TG + 1], st));
+                FLC_CHECK_HIP(hipStreamWaitEvent(sside, cx->ev[TG + 1], 0));
+            }
+            sample(0, rs1, st);
+            FLC_CHECK_LAUNCH("k_topk_sample");
+            if (split) {
+                sample(rs1, n, sside);
+                FLC_CHECK_LAUNCH("k_topk_sample (side)");
+                FLC_CHECK_HIP(hipEventRecord(cx->ev[TG + 2], sside));
+            }
             for (int g = 0; g < TG; ++g) {
                 const int64_t r0 = group_row(n, TG, g, FLC_TK_LASTPCT), rn = group_row(n, TG, g + 1, FLC_TK_LASTPCT) - r0;
+                if (split && g == 1) FLC_CHECK_HIP(hipStreamWaitEvent(st, cx->ev[TG + 2], 0));
                 { ProfScope _ps("k_topk_filter", st);
                 // few rows: 2-chunk groups (twice the waves in flight for a lone row)
                 // (one-chunk items for a lone 10 M row measured slower: 26 -> 36 us)
