@@ -64,6 +64,9 @@ constexpr int DS_NH = 2 * DS_FGS;          // fold tiles (half chunks) per item
 constexpr int DS_GCAP = 512;               // staged candidates per item (6.25 %; more -> row overflow)
 constexpr int DS_HCAP = DS_GCAP / DS_NH;    // entries per half chunk of an item (more -> row overflow)
 constexpr int DS_MAXLEV = 15;              // entry level field: 4 bits (a higher level -> row dense)
+#ifndef FLC_DS_SPLIT_SAMPLE
+#define FLC_DS_SPLIT_SAMPLE 1         // QSGD row groups: only group 0's sample before the first filter
+#endif
 #ifndef FLC_DS_SMAX
 #define FLC_DS_SMAX 65536
 #endif
@@ -140,11 +143,11 @@ __device__ inline float f32_down(double v) { float f = (float)v; return (double)
 // Sample: one workgroup per row.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(DS_SNT) void k_ds_sample(RowSrc rows, int64_t n, int64_t d, const float* __restrict__ levels,
-                                                      int s, uint64_t seed, int64_t client0, DsWs ws) {
+                                                      int s, uint64_t seed, int64_t client0, DsWs ws, int64_t r_off) {
     constexpr int NW = DS_SNT / 64;
     __shared__ double r2[NW], r4[NW];
-    const int64_t row = blockIdx.x;
-    if (blockIdx.x == 0) load_table(levels, s, ws.gtab);
+    const int64_t row = r_off + blockIdx.x;                               // (a launch may take a row range)
+    if (row == 0) load_table(levels, s, ws.gtab);
     if (row >= n) return;
     const float* r = rows.row(row);
     double a2 = 0.0, a4 = 0.0;
@@ -1785,10 +1788,20 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         return FLC_OK;
     };
 
-    { ProfScope _ps("k_ds_sample", st);
-    hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)n), dim3(DS_SNT), 0, st, rows, n, d, prm->d_levels, prm->s, prm->seed, client0, ws); }
-    FLC_CHECK_LAUNCH("k_ds_sample");
+    auto sample = [&](int64_t a, int64_t b, hipStream_t sx) -> int {
+        if (b <= a) return FLC_OK;
+        ProfScope _ps("k_ds_sample", sx);
+        hipLaunchKernelGGL(k_ds_sample, dim3((unsigned)(b - a)), dim3(DS_SNT), 0, sx, rows, n, d, prm->d_levels, prm->s, prm->seed,
+                           client0, ws, a);
+        FLC_CHECK_LAUNCH("k_ds_sample");
+        return FLC_OK;
+    };
     const int TO = tail_groups(n);
+    // row groups (K >= 2): only group 0's sample before its filter; the other rows' samples run on
+    // the side stream beside it and group 1's filter waits for them
+    const bool split = FLC_DS_SPLIT_SAMPLE && K >= 2;
+    if (!split)
+        if (int rc = sample(0, n, st)) return rc;
     if (K == 1 && TO <= 1) {
         int rc = filter(0, n);
         if (rc) return rc;
@@ -1807,7 +1820,7 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         FLC_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         FLC_CHECK_HIP(hipStreamCreateWithPriority(&cx.side, hipStreamNonBlocking, hi));
     }
-    while ((int)cx.ev.size() < std::max(K, TO) + 2) {
+    while ((int)cx.ev.size() < std::max(K, TO) + 4) {
         hipEvent_t e;
         FLC_CHECK_HIP(hipEventCreateWithFlags(&e, FLC_SYNC_EVENT_FLAGS));
         cx.ev.push_back(e);
@@ -1826,8 +1839,18 @@ int ds_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, int
         FLC_CHECK_HIP(hipStreamWaitEvent(st, cx.ev[TO], 0));
         return accum(0, n, 1, 1, st);
     }
+    const int EV_S0 = std::max(K, TO) + 2, EV_S1 = EV_S0 + 1;
+    if (split) {
+        const int64_t rs1 = group_row(n, K, 1, FLC_DS_LASTPCT);
+        FLC_CHECK_HIP(hipEventRecord(cx.ev[EV_S0], st));                   // after the work queued before
+        FLC_CHECK_HIP(hipStreamWaitEvent(cx.side, cx.ev[EV_S0], 0));
+        if (int rc = sample(0, rs1, st)) return rc;
+        if (int rc = sample(rs1, n, cx.side)) return rc;
+        FLC_CHECK_HIP(hipEventRecord(cx.ev[EV_S1], cx.side));
+    }
     for (int g = 0; g < K; ++g) {
         const int64_t r0 = group_row(n, K, g, FLC_DS_LASTPCT), r1 = group_row(n, K, g + 1, FLC_DS_LASTPCT);
+        if (split && g == 1) FLC_CHECK_HIP(hipStreamWaitEvent(st, cx.ev[EV_S1], 0));
         int rc;
         if (FLC_DS_RG_SIDE) {
             // the group's whole tail (norm, resolve, fold) on the side stream, under the next
