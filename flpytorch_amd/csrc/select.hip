@@ -163,6 +163,52 @@ __device__ inline void hist_find_at(const uint32_t* h, uint32_t k, uint32_t& bin
     above = scratch[257];
     __syncthreads();
 }
+// The same search over NB bins (NB / 256 a thread, threads 0..255 of a larger block; the rest only
+// sync); found = false when the bins hold fewer than k in all.
+template <int NB>
+__device__ inline void hist_find_n(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above, bool& found,
+                                   uint32_t* scratch /* LDS 256+3 */) {
+    constexpr int PER = NB / 256;
+    static_assert(NB % 256 == 0, "256 threads scan NB / 256 bins each");
+    const int t = (int)threadIdx.x;
+    const bool own = t < 256;
+    uint32_t local[PER];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) { local[q] = own ? h[NB - 1 - (t * PER + q)] : 0u; s += local[q]; }
+    if (t == 0) { scratch[256] = 0; scratch[257] = 0; scratch[258] = 0; }
+    const int lane = t & 63, w = t >> 6;
+    uint32_t inc = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off, 64);
+        inc += lane >= off ? v : 0u;
+    }
+    if (own && lane == 63) scratch[w] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    if (own)
+        for (int q = 0; q < w; ++q) before += scratch[q];
+    const uint32_t incl = own ? before + inc : 0u, excl = incl - s;
+    if (own && excl < k && incl >= k) {
+        uint32_t run = excl;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            if (run + local[q] >= k) {
+                scratch[256] = (uint32_t)(NB - 1 - (t * PER + q));
+                scratch[257] = run;
+                scratch[258] = 1;
+                break;
+            }
+            run += local[q];
+        }
+    }
+    __syncthreads();
+    bin = scratch[256];
+    above = scratch[257];
+    found = scratch[258] != 0u;
+    __syncthreads();
+}
 __device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
                                  uint32_t* scratch /* LDS 256+2 */) {
     hist_find_at(h, k, bin, above, scratch, (int)threadIdx.x, threadIdx.x < 256);   // larger blocks: the rest only sync
@@ -2549,9 +2595,6 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             // from its histogram — both digits in ONE round
             RS_STAMP(2);
             uint32_t* s0 = ctl + RS_HSPEC;
-            if (t < 4) scratch[4 + t] = 0;
-            __syncthreads();
-            uint32_t cw[3] = {0u, 0u, 0u};
             for (int i = t; i < HBINS; i += RS_NT) {
 #pragma unroll
                 for (int w = 0; w < 3; ++w) {
@@ -2562,39 +2605,27 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                         c += __hip_atomic_load(sw + r * 3 * HBINS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (i == 0 && bs + (uint32_t)w == 1u) c -= pad;         // the padding: first digit 0, second 0
                     h1[w * HBINS + i] = c;
-                    cw[w] += c;
                 }
             }
-            uint32_t A = 0;
-            if (t == 0)
+            if (t == 0) {
+                uint32_t A = 0;
 #pragma unroll
                 for (int r = 0; r < RS_NG; ++r) A += __hip_atomic_load(ctl + RS_ABV + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int w = 0; w < 3; ++w) {
-                const uint32_t c = wave_sum(cw[w]);
-                if ((t & 63) == 0 && c) atomicAdd(&scratch[4 + w], c);
+                scratch[259] = A;
             }
-            if (t == 0) scratch[7] = A;
             __syncthreads();
-            A = scratch[7];
-            const uint32_t c0 = scratch[4], c1 = scratch[5], c2 = scratch[6];
-            __syncthreads();
-            // windows from the top: bs + 1 (w 2), bs (w 1), bs - 1 (w 0)
-            int w0 = -1;
-            uint32_t a0 = A;
-            if (A < (uint32_t)K) {
-                if (A + c2 >= (uint32_t)K) w0 = 2;
-                else if (A + c2 + c1 >= (uint32_t)K) { w0 = 1; a0 = A + c2; }
-                else if (A + c2 + c1 + c0 >= (uint32_t)K) { w0 = 0; a0 = A + c2 + c1; }
-            }
+            const uint32_t A = scratch[259];
+            // the three windows in index order w 0, 1, 2 are first digits bs - 1, bs, bs + 1: from the
+            // top, h1's 3 x 2048 bins descend through both digits at once — one search finds both
+            uint32_t bb = 0, ab = 0;
+            bool found = false;
+            if (A < (uint32_t)K) hist_find_n<3 * HBINS>(h1, (uint32_t)K - A, bb, ab, found, scratch);   // (uniform)
             uint64_t pl = 0;                                             // miss: start from the first digit
-            if (w0 >= 0) {                                               // (uniform)
-                uint32_t b1, a1;
-                hist_find(h1 + w0 * HBINS, (uint32_t)K - a0, b1, a1, scratch);
-                const uint32_t b0 = bs - 1u + (uint32_t)w0;
+            if (found) {
+                const uint32_t w0 = bb / HBINS, b1 = bb % HBINS, b0 = bs - 1u + w0;
                 // hit | 22-bit prefix << 1 | krem << 23 | the prefix's count (saturated) << 47
-                pl = 1ull | ((uint64_t)((b0 << 11) | b1) << 1) | ((uint64_t)((uint32_t)K - a0 - a1) << 23) |
-                     ((uint64_t)min(h1[w0 * HBINS + b1], 16383u) << 47);
+                pl = 1ull | ((uint64_t)((b0 << 11) | b1) << 1) | ((uint64_t)((uint32_t)K - A - ab) << 23) |
+                     ((uint64_t)min(h1[bb], 16383u) << 47);
             }
             rs_release(tr, &gen_s, pl);
             if (t == 0) { scratch[0] = (uint32_t)pl; scratch[1] = (uint32_t)(pl >> 32); }
