@@ -184,3 +184,29 @@ def test_compressvector_resident_edges(ag, d, kind):
         assert not f & 1, f"{tie}: flags {f} (a barrier gave up)"
         if d <= 16_777_216 and d * 4 < 2**31:
             assert f & 16, f"{tie}: flags {f}, expected the register-resident select"
+
+
+@pytest.mark.parametrize("where", ["between_pieces", "in_pieces"])
+def test_compressvector_resident_speculation_miss(ag, where):
+    """k_lone_resident guesses the K-th key's first digit from a fixed sample (32 pieces of 256
+    elements spread over the row) and takes both digits from one round when the guess holds.  Rows
+    built so that the sample misjudges the row: the large magnitudes only BETWEEN the sampled pieces
+    (the sample sees none of them: the guess is far too low), or only INSIDE them (far too high).
+    The result must not depend on the guess: bit-exact vs the oracle under both tie rules."""
+    d = 4_000_003
+    k = 40_000
+    g = np.random.default_rng([d, len(where)])
+    x = (g.standard_normal(d) * 1e-3).astype(np.float32)
+    inside = np.zeros(d, dtype=bool)
+    for p in range(32):
+        a = p * (d - 256) // 31
+        inside[a:a + 256] = True
+    pool = np.flatnonzero(~inside if where == "between_pieces" else inside)
+    big = g.choice(pool, size=min(2 * k, pool.size), replace=False)
+    x[big] = (g.standard_normal(big.size) * 10.0).astype(np.float32)
+    xt = torch.from_numpy(x).cuda()
+    for tie in ("lowest", "highest"):
+        c = _comp(ag, f"topk:{k}", d, tie)
+        np.testing.assert_array_equal(_bits(c.compressVector(xt)), _bits(_enc([x], k, tie)[0]), err_msg=tie)
+        f = int(ag.select_row_flags(c, 1, d)[0])
+        assert f & 16 and not f & 1, f"{tie}: flags {f}"
