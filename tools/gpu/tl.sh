@@ -19,7 +19,7 @@ for cs in "$@"; do
       python3 $root/bench.py --workload $wl --steps 4 --warmup 2 --no-cpu-baseline $rg > $o/bench_$name.log 2>&1 ) || exit 1
   cd $root
   { echo "== $cs"; grep -h '^{' $o/bench_$name.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('ms_per_step', d['ms_per_step'])"; \
-    python3 tools/timeline.py $o/tr_$name $first 2; } >> $o/tl_$wl.txt
+    python3 tools/timeline.py $o/tr_$name $first 2 $([ "$wl" = c3 ] || [ "$wl" = c4 ] && echo 2 || echo 1); } >> $o/tl_$wl.txt
   rm -rf $o/tr_$name
 done
 cat $o/tl_$wl.txt

@@ -1,7 +1,7 @@
 """One step's kernel timeline from a rocprofv3 --kernel-trace CSV: every kernel from the last
 launch of the step's first kernel (default k_ds_sample) on, start / end in us from that launch.
 
-usage: python tools/timeline.py <dir with *kernel_trace.csv> [first-kernel-substring] [nth-from-last]
+usage: python tools/timeline.py <dir with *kernel_trace.csv> [first-kernel-substring] [nth-from-last] [launches per step]
 """
 import csv
 import glob
@@ -16,6 +16,8 @@ f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
 rows = list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
+stride = int(sys.argv[4]) if len(sys.argv) > 4 else 1      # launches of the first kernel per step
+starts = starts[::stride]
 i0 = starts[-nth]
 i1 = starts[-nth + 1] if nth > 1 else len(rows)
 t0 = int(rows[i0]["Start_Timestamp"])
