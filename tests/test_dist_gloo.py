@@ -232,3 +232,31 @@ def test_mixed_uplink_groups():
     with pytest.raises(ValueError):
         up.groups(4, 3)
     assert len(set(up.seeds)) == 3
+
+
+def _mean_bound_check(out, enc, n):
+    """SURVEY §8d reduction tolerance: |build - fp64 mean| <= (ceil(log2 N) + 2) 2^-24 mean|.|
+    elementwise (mean|.| = the fp64 mean of the encodings' magnitudes at that element)."""
+    e64 = np.stack(enc).astype(np.float64)
+    mean64 = e64.sum(0) / n
+    mabs = np.abs(e64).sum(0) / n
+    bound = (int(np.ceil(np.log2(n))) + 2) * 2.0 ** -24 * mabs
+    err = np.abs(out.astype(np.float64) - mean64)
+    assert np.all(err <= bound), (float((err - bound).max()), int(np.argmax(err - bound)))
+    return float((err / np.where(bound > 0, bound, 1.0)).max())
+
+
+@pytest.mark.parametrize("world,mode", [(2, "allreduce"), (4, "allreduce"), (2, "ordered"), (4, "ordered")])
+def test_sharded_mean_within_survey_bound(world, mode):
+    """Both combines against the fp64 mean under SURVEY §8d's (ceil(log2 N)+2) 2^-24 bound (not only
+    against one process's fp32 result), N = 37 clients over 2 / 4 ranks."""
+    spec, n, d = "topk:5%", 37, 4099
+    res = _run(world, spec, n, d, mode)
+    rows = make_rows(n, d)
+    enc = [oc.OracleCompressor(spec, d).compress(rows[i]) for i in range(n)]
+    for r in range(world):
+        np.testing.assert_array_equal(res[r], res[0])
+    used = _mean_bound_check(res[0], enc, n)
+    seq = oc.reduce_plain(enc)                                    # the reference's sequential fold
+    ulp = int(np.abs(res[0].view(np.int32).astype(np.int64) - seq.view(np.int32).astype(np.int64)).max())
+    print(f"world {world} {mode}: max err / bound {used:.3f}, max ulp vs sequential {ulp}")

@@ -109,6 +109,16 @@ def test_two_ranks_hip_encoder(spec, mode):
     w = want.cpu().numpy()
     bad = np.flatnonzero(_bits(got) != _bits(w))
     assert bad.size == 0, f"{bad.size} of {d} differ, first {bad[:5]}: {got[bad[:5]]} vs {w[bad[:5]]}"
+    if spec.startswith("topk"):
+        # the HIP-encoded 2-rank mean against the fp64 mean of the oracle's encodings,
+        # |build - mean64| <= (ceil(log2 N) + 2) 2^-24 mean|.| elementwise (TopK: deterministic
+        # encodings, so the oracle's are the clients' own)
+        from oracle import codecs as oc
+        rows_h = _rows(n, d).numpy()
+        e64 = np.stack([oc.OracleCompressor(spec, d).compress(rows_h[i]) for i in range(n)]).astype(np.float64)
+        bound = (int(np.ceil(np.log2(n))) + 2) * 2.0 ** -24 * np.abs(e64).sum(0) / n
+        err = np.abs(got.astype(np.float64) - e64.sum(0) / n)
+        assert np.all(err <= bound), (float((err - bound).max()), int(np.argmax(err - bound)))
 
 
 def _bench(args, timeout=200):
