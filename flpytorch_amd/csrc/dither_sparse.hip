@@ -96,6 +96,12 @@ constexpr int DS_RINGC = 4;                // compat filter ring (x + u: 24 B pe
 #define FLC_DS_PL 0
 #endif
 constexpr int DS_PLS = 10;
+#ifndef FLC_DS_STPOL
+// k_ds_filter's list copy-outs (sure and ambiguous entries) as nontemporal stores: bit-identical,
+// C4 9.736 -> 9.615 ms per step on one allocation (profiles/r05/ab_list_stnt.txt; the same for
+// the TopK filter's lists ran 7.618 -> 7.734 ms at C3, so FLC_TK_STPOL stays 0)
+#define FLC_DS_STPOL 2
+#endif
 #ifndef FLC_DS_CU
 #define FLC_DS_CU 2                  // k_ds_filter: candidate batches (of 64) classified per iteration
 #endif
@@ -621,7 +627,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
                                                               (int)((NH - 1) * hstride + DS_HCAP * 2), 0x00020000);
             const uint4 v = reinterpret_cast<const uint4*>(s16)[lane];
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od,
-                                                   put ? u * hstride + k8 * 2u : 0x7FFFFFF0u, 0, 0);
+                                                   put ? u * hstride + k8 * 2u : 0x7FFFFFF0u, 0, FLC_DS_STPOL);
         }
         {
             // ambiguous entries: two per lane per 16-B store; an odd count's last slot is stale
@@ -632,7 +638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMPAT ? FL
             for (int k = 0; k < GCAP / 128; ++k) {
                 const uint4 v = sq[k * 64 + lane];
                 __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od, (k * 64 + lane) * 16, 0, 0);
+                    __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), od, (k * 64 + lane) * 16, 0, FLC_DS_STPOL);
             }
         }
         // the copy-out reads precede the next item's staging writes in the wave's program order

@@ -875,6 +875,9 @@ template <int RING, int FGS, int LONE = 0>
 #ifndef FLC_TK_RING
 #define FLC_TK_RING 16               // loads in flight per wave (ring registers: 4 x RING VGPRs)
 #endif
+#ifndef FLC_TK_STPOL
+#define FLC_TK_STPOL 0               // A/B: the filter's list copy-out stores nontemporal (2) or default (0)
+#endif
 #ifndef FLC_TK_COPY4
 #define FLC_TK_COPY4 1               // TopK filter copy-out: 16-B stores of whole quads
 #endif
@@ -971,13 +974,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLC_TK_WPE)
                 const uint4 a = reinterpret_cast<const uint4*>(si)[q];
                 const uint4 b = reinterpret_cast<const uint4*>(sv)[q];
                 const uint32_t off = q < nq ? q * 16u : 0x7FFFFFF0u;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), di, off, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), dv, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), di, off, 0, FLC_TK_STPOL);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), dv, off, 0, FLC_TK_STPOL);
             }
             const uint32_t e = nq * 4u + (uint32_t)(lane & 3);          // the partial quad (range-checked)
             const uint32_t off = lane < 3 ? e * 4u : 0x7FFFFFF0u;
-            __builtin_amdgcn_raw_buffer_store_b32(si[e], di, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(sv[e], dv, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(si[e], di, off, 0, FLC_TK_STPOL);
+            __builtin_amdgcn_raw_buffer_store_b32(sv[e], dv, off, 0, FLC_TK_STPOL);
         }
 #else
         if (fits && FLC_TK_PROBE != 2) {
