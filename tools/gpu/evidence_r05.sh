@@ -7,9 +7,12 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 out=gpurun_out/${EV_OUT:-ev_r05}
 mkdir -p $out
+# EV_SKIP_TESTS=1: the suite already ran on this build in an earlier call (its log is copied in)
+if [ -z "$EV_SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
     --timeout-method thread -rf > $out/gpu_tests.log 2>&1 || exit $?
 echo "tests: $(tail -1 $out/gpu_tests.log)"
+fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit $?
 for wl in c3 c4 c2; do
   timeout -k 10 400 python tools/collect_pmc.py --workload $wl > $out/pmc_$wl.log 2>&1 || exit $?
