@@ -411,8 +411,12 @@ def dropin(args):
     rows = torch.randn(n, d, generator=gen, device=dev)
     x = torch.zeros(d, device=dev)
     comps = [ag.initCompressor(spec, d) for _ in range(n)]
+    for c in comps:
+        # "torch_cpu": the reference's own norm bits (torch's CPU order, k_norm_torch) — the price
+        # of bit-exact dithering through install()
+        c.norm_mode = args.norm_mode
     rs = np.random.RandomState(123)
-    dither = spec.startswith(("qsgd", "std_dithering", "natural", "terngrad"))
+    dither = spec.startswith(("qsgd", "std.dithering", "nat.dithering", "natural", "terngrad"))
     for i in range(n):                              # compat patterns drawn once (host numpy stream)
         comps[i].generateCompressPattern(rs, "cuda", i, {})
 
@@ -473,7 +477,7 @@ def dropin(args):
     # per-kernel device time of one compressVector, over every client's row (flc_profile scopes)
     kernels = ["k_topk_sample", "k_topk_filter", "k_cand_select", "k_topk_exact_rows", "k_chunk_accum",
                "k_norm_partials", "k_ew_accum_vec", "k_ew_encode", "k_randk_scatter_dev", "k_assign_scatter",
-               "k_assign_finish", "k_lone_dither", "k_lone_resident"]
+               "k_assign_finish", "k_lone_dither", "k_lone_resident", "k_norm_torch"]
     _lib.profile_enable(True)
     for k in kernels:
         _lib.profile_collect(k)
@@ -494,11 +498,12 @@ def dropin(args):
         with open(pmc) as f:
             pj = json.load(f)
         cv_kernel = pj.get("kernel")
-        if cv_kernel and any(cv_kernel in k for k in per_kernel):
+        # the same compressVector kernel at the same D
+        if cv_kernel and any(cv_kernel in k for k in per_kernel) and pj.get("d") == d and args.norm_mode == "exact":
             cv_traffic = pj.get("hbm_bytes_per_launch")
     print(json.dumps({"metric": "drop-in compressVector + serverGradient fold, device time; % HBM peak",
                       "mode": "drop-in path (compressVector per client + serverGradient fold) vs fused uplink",
-                      "codec": spec, "clients": n, "D": d,
+                      "codec": spec, "clients": n, "D": d, "norm_mode": args.norm_mode,
                       "roofline": {"bound": "hbm", "kernel": "compressVector (one row)", "achieved": cv["GBps"],
                                    "peak": PEAK_GBS, "unit": "GB/s", "frac": cv["frac"], "traffic": cv_traffic,
                                    "traffic_unit": "HBM bytes per launch of " + str(cv_kernel) + " (rocprofv3 PMC, profiles/)",
@@ -564,6 +569,60 @@ def dist_info(dist, dev, d, reps=5):
             "distinct_devices": len({(r["host"], r["pci_bus_id"], r["device"]) for r in ranks}),
             "allreduce_bytes": nbytes, "allreduce_ms": round(ms, 4),
             "allreduce_busbw_GBps": round(2.0 * (g - 1) / g * nbytes / (ms * 1e-3) / 1e9, 3) if ms > 0 else None}
+
+
+def strong_block(encode_partial, fold, block_rows, n_total, d, dev, steps, warmup, group=None):
+    """The north_star's scaling measurement on every line: C4 at FIXED N
+    (n_total clients, qsgd:127 on the GPU) in the 8 fixed client blocks of sharding.py, rank r of G
+    owning blocks r*8/G .., every block encoded into its own exact partial, the partials combined in
+    block order ("ordered": all-to-all + block-order fold + all-gather), so the [D] result has the
+    same bits at G = 1, 2, 4, 8.  Every rank holds the same resident block of rows (block_rows:
+    n_total / 8 rows, identical on every rank) and replays it for each of its blocks with the
+    block's own client ids (its own device-RNG draws): the work of a block does not depend on G.
+    Returns ms per step (max over ranks, barrier + sync around exactly `steps` steps), the
+    whole-job rate 4 n_total D + 4 D bytes / step, and the sha256 of the result's bytes, from which
+    a SCALE run reads both the speed-up and the G-invariance.  Collective: every rank calls it."""
+    import hashlib
+    import torch.distributed as dist
+    from flpytorch_amd.sharding import N_BLOCKS, ShardedUplink, rank_clients
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    r_lo, r_hi = rank_clients(n_total, world, rank)
+    uplink = ShardedUplink(encode_partial, group=group, mode="ordered", fold=fold)
+    out = torch.empty(d, dtype=torch.float32, device=dev)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier(group)
+
+    def step():
+        uplink(lambda lo, hi: block_rows[:hi - lo], client0=r_lo, total_weight=float(n_total), n_clients=n_total,
+               out=out, d=d, device=dev)
+    for _ in range(warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        elapsed = float(t.item())
+    ms = elapsed / steps * 1e3
+    nbytes = 4 * n_total * d + 4 * d
+    digest = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
+    return {"workload": f"C4 qsgd:127 N={n_total} (fixed) D={d}, {N_BLOCKS} client blocks, ordered combine",
+            "n_gpus": world, "clients_total": n_total, "clients_per_gpu": r_hi - r_lo, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(ms, 4), "value_GBps": round(nbytes / (ms * 1e-3) / 1e9, 2),
+            "pct_hbm_peak_per_gpu": round(100.0 * nbytes / (ms * 1e-3) / 1e9 / world / PEAK_GBS, 2),
+            "result_sha256": digest,
+            "scaling": "strong (fixed N; speed-up = this line's ms_per_step at G=1 / at G)",
+            "rows": f"{block_rows.shape[0]} resident rows per GPU (one fixed-seed block, the same on every rank) "
+                    "replayed for each of the rank's blocks with the block's client ids"}
 
 
 def launch_ranks(gpus, cmd, poll_s=0.2, grace_s=10.0):
@@ -634,6 +693,11 @@ def main():
                     help="per-client compressVector + serverGradient fold (the install() path) vs the fused uplink")
     ap.add_argument("--wire", action="store_true",
                     help="server side from the wire format: decode+reduce of N resident payloads (own line, not value)")
+    ap.add_argument("--norm-mode", default="exact", choices=["exact", "torch_cpu"],
+                    help="--dropin: Compressor.norm_mode of the dithering codecs (torch_cpu: the reference's norm bits)")
+    ap.add_argument("--no-strong-c4", action="store_true",
+                    help="skip the strong_c4 block (C4 at fixed N=4096, ordered combine) of the default line")
+    ap.add_argument("--strong-steps", type=int, default=5, help="timed steps of the strong_c4 block")
     ap.add_argument("--e2e", action="store_true",
                     help="end-to-end: client rows start in pinned host memory, the [D] result lands in host memory "
                          "(H2D + encode+reduce + D2H per step; PCIe-bound; reported in DESIGN.md, never as value)")
@@ -845,6 +909,24 @@ def main():
         elapsed = float(t.item())
     ceiling = read_ceiling(rows, out)
     mg = dist_info(dist, dev, d) if world > 1 else None
+    strong_c4 = None
+    if args.workload == "c3" and not (args.no_strong_c4 or args.compat or strong or args.d):
+        # the north_star's fixed-N scaling curve (C4, N=4096) on every default line, G = 1 included:
+        # the C3 rows are released first (51.2 GB of C4 block rows + its workspace instead)
+        del rows
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        from flpytorch_amd.sharding import N_BLOCKS, product_fold, product_partial
+        c4 = WORKLOADS["c4"]
+        blk = c4["n_total"] // N_BLOCKS
+        g4 = torch.Generator(device=dev).manual_seed(4096)          # the same rows on every rank
+        rows4 = torch.empty((blk, c4["d"]), dtype=torch.float32, device=dev)
+        for i in range(0, blk, 64):
+            rows4[i:i + 64].normal_(generator=g4)
+        red4 = ag.UplinkReducer(ag.initCompressor(c4["spec"], c4["d"]), device=dev, seed=20241015)
+        strong_c4 = strong_block(product_partial(red4), product_fold(), rows4, c4["n_total"], c4["d"], dev,
+                                 steps=args.strong_steps, warmup=1, group=dist.group.WORLD if world > 1 else None)
+        del rows4
 
     step_ms = elapsed / args.steps * 1e3
     total_bytes = algorithmic_bytes(spec, n_total, d, k) if strong else algorithmic_bytes(spec, n, d, k, specs) * world
@@ -877,22 +959,29 @@ def main():
         pmc_rk = os.path.join(ROOT, "profiles", "pmc_c5_randk.json")
         if os.path.exists(pmc_rk):
             with open(pmc_rk) as f:
-                rk_traffic = json.load(f).get("hbm_bytes_per_launch")
+                pr = json.load(f)
+            if pr.get("n") == n and pr.get("d") == d:            # (a pass of this line's shape only)
+                rk_traffic = pr.get("hbm_bytes_per_launch")
         if rk_ms:
             randk_group = {"rows": nr, "ms_per_step": round(rk_ms, 4),
                            "algorithmic_GBps": round((4 * nr * k + 4 * d) / (rk_ms * 1e-3) / 1e9, 1),
                            "line_floor_bytes": int(rk_floor),
                            "line_floor_GBps": round(rk_floor / (rk_ms * 1e-3) / 1e9, 1),
                            "fold_traffic_bytes": rk_traffic}
-    traffic = None
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{'_compat' if args.compat else ''}.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and not strong:
         with open(pmc) as f:
             pj = json.load(f)
-        # only the PMC pass of this line's dominant kernel and pattern source (a compat line's
-        # filter also reads the uniforms)
-        if wl["kernel"] in pj.get("kernel", "") and bool(pj.get("compat")) == bool(args.compat):
+        # only a PMC pass of this line's shape: the same dominant kernel and
+        # pattern source (a compat line's filter also reads the uniforms), rows per GPU, D and
+        # launches per step — counters of another shape would price other bytes per launch
+        if (wl["kernel"] in pj.get("kernel", "") and bool(pj.get("compat")) == bool(args.compat)
+                and pj.get("n") == n and pj.get("d") == d and pj.get("launches_per_step") is not None
+                and abs(pj["launches_per_step"] - launches_per_step) < 0.01):
             traffic = pj.get("hbm_bytes_per_launch")
+            traffic_src = {"file": os.path.relpath(pmc, ROOT), "n": pj["n"], "d": pj["d"],
+                           "launches_per_step": pj["launches_per_step"]}
 
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(spec, d, n_total if strong else n * world,
@@ -935,6 +1024,7 @@ def main():
                          # traffic: PMC HBM bytes of ONE launch (the contract's unit, like avg_launch_ms);
                          # beside it the algorithmic bytes of one launch and their ratio, then the step's
                          "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": int(kb_launch) if kb_launch else None,
                          "traffic_over_algorithmic": round(traffic / kb_launch, 4) if (traffic and kb_launch) else None,
                          "traffic_per_step": int(traffic * launches_per_step) if (traffic and klaunch) else None,
@@ -954,6 +1044,8 @@ def main():
         }
         if randk_group:
             line["randk_group"] = randk_group
+        if strong_c4:
+            line["strong_c4"] = strong_c4
         if mg:
             line["multi_gpu"] = mg
         print(json.dumps(line), flush=True)

@@ -22,7 +22,7 @@ FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
 # execution hints (flc_codec_params.flags): how, never what — every choice gives the same bits
 FLC_PATH_AUTO, FLC_PATH_SPARSE, FLC_PATH_DENSE = 0, 1, 2
 FLC_TIE_LOWEST, FLC_TIE_HIGHEST = 0, 1
-ABI_VERSION = 101
+ABI_VERSION = 102
 
 
 def FLC_ROW_GROUPS(g):
@@ -43,7 +43,7 @@ EXPORTS = [
     "flc_device_uniform", "flc_device_randk_indices",
     "flc_device_randk_counts_workspace_size", "flc_device_randk_counts",
     "flc_profile_enable", "flc_profile_collect", "flc_select_row_flags",
-    "flc_selftest_division", "flc_norm2_torch_cpu",
+    "flc_selftest_division", "flc_norm2_torch_cpu", "flc_debug_resident",
 ]
 
 
@@ -178,6 +178,8 @@ def _bind(lib):
     lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
     if hasattr(lib, "flc_norm2_torch_cpu"):         # (absent from A/B builds of older revisions)
         lib.flc_norm2_torch_cpu.argtypes = [vp, i64, i64, i64, vp, vp]
+    if hasattr(lib, "flc_debug_resident"):          # (absent from A/B builds of older revisions)
+        lib.flc_debug_resident.argtypes = [i32, i64]
     if hasattr(lib, "flc_select_row_flags"):        # (absent from A/B builds of older revisions)
         lib.flc_select_row_flags.argtypes = [P(FlcCodecParams), i64, i64, vp, sz, vp, vp]
     for name in EXPORTS:

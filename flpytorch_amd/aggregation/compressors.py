@@ -144,8 +144,10 @@ class Compressor:
         # what (not how): the p = 2 norm of standard dithering / QSGD in compressVector —
         #   "exact"      the correctly rounded norm (default; deterministic on every host)
         #   "torch_cpu"  the reference's own fp32 value, torch.norm(x, p=2) on a CPU tensor
-        #                (compressors.py:272) in torch's CPU reduction order, bit for bit
-        #                (flc_norm2_torch_cpu; latency-bound: ~ms per row at D = 25 M)
+        #                (compressors.py:272 / 303: standard and natural dithering) in torch's CPU
+        #                reduction order, bit for bit on x86 hosts with AVX2 (torch's 8-lane AVX2
+        #                norm kernel, which AVX512 hosts run too; without AVX2: unpinned)
+        #                (flc_norm2_torch_cpu; latency-bound: see bench.py --dropin --norm-mode)
         self.norm_mode = "exact"
         # what: TopK's choice among entries tied at the K-th magnitude when fewer places are left
         # than ties (compressors.py:332 leaves it to torch.topk) — "lowest" indices (default: the
@@ -344,7 +346,10 @@ class Compressor:
         mode = getattr(self, "norm_mode", "exact")
         if mode not in ("exact", "torch_cpu"):
             raise ValueError(f"norm_mode must be 'exact' or 'torch_cpu' (got {mode!r})")
-        if mode == "exact" or self.compressorType != CompressorType.STANDARD_DITHERING_FP32:
+        # standard dithering / QSGD (compressors.py:272) and natural dithering (303, whose output
+        # y * sign * pnorm carries the norm's bits) both take torch.norm(x, p)
+        if mode == "exact" or self.compressorType not in (CompressorType.STANDARD_DITHERING_FP32,
+                                                          CompressorType.NATURAL_DITHERING_FP32):
             return False
         if self.p == 2:
             return True

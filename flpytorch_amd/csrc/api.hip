@@ -72,7 +72,7 @@ static int bad_params(const flc_codec_params* prm, const char* what) {
 
 using namespace flc;
 
-extern "C" int flc_version(void) { return 101; }   // 1.01: flc_codec_params.tie, flc_norm2_torch_cpu
+extern "C" int flc_version(void) { return 102; }   // 1.02: flc_debug_resident (1.01: flc_codec_params.tie, flc_norm2_torch_cpu)
 
 #ifndef FLC_SRC_HASH
 #define FLC_SRC_HASH "unknown"
@@ -116,6 +116,8 @@ extern "C" int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int6
     if (!prm || (n > 0 && (!d_workspace || !d_flags))) { set_error("flc_select_row_flags: null argument"); return FLC_ERR_ARG; }
     return sel_row_flags(prm, n, d, d_workspace, ws_bytes, d_flags, (hipStream_t)stream);
 }
+
+extern "C" int flc_debug_resident(int grid_mult, int64_t spin_ticks) { return rs_debug(grid_mult, spin_ticks); }
 
 extern "C" int flc_norm2_torch_cpu(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* stream) {
     if (n < 0 || d < 0 || (n > 1 && ld < d) || (n > 0 && (!d_rows || !d_out))) {

@@ -181,6 +181,7 @@ int norm_torch_run(const float* x, int64_t ld, int64_t n, int64_t d, float* out,
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st);
+int rs_debug(int mult, int64_t spin_ticks);
 int sel_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* wsp, size_t ws_bytes,
                   uint32_t* flags, hipStream_t st);
 bool ds_eligible(const flc_codec_params* prm, const flc_pattern* pat, int64_t n, int64_t d);

@@ -29,6 +29,7 @@
 // Keys: |x| bits with the sign cleared (uint32, monotone; NaN above inf like torch.topk).
 #include <stdlib.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -41,6 +42,7 @@ namespace flc {
 constexpr uint32_t ALL = 0xFFFFFFFFu;
 constexpr uint32_t F_OVERFLOW = 1u, F_SHORT = 2u, F_TIES = 4u, F_EXACT = 8u;
 constexpr uint32_t F_RESIDENT = 16u;  // a lone row selected exactly in registers (k_lone_resident)
+constexpr uint32_t F_REPAIR = 32u;    // ... whose grid was not co-resident: re-selected by its last workgroup
 constexpr int SMAX = 16384;          // sample size kept in LDS
 constexpr int HBINS = 2048;          // radix histogram bins (11 bits)
 constexpr uint32_t TIECAP = HBINS;   // fast-path tie list (LDS); more ties at the K-th key -> exact path
@@ -56,12 +58,25 @@ constexpr int RS_NG = FLC_RS_NG;
 constexpr int RS_NG_MAX = 16;
 static_assert(RS_NG >= 1 && RS_NG <= RS_NG_MAX, "FLC_RS_NG: 1..16 groups");
 // its control words: counters on lines of their own, per-group digit histograms, tie counts
-constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128;
+// (RS_GAVE: the sequence number of a call that was aborted; RS_EXIT: workgroups that have left)
+constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_EXIT = 128, RS_GRP = 160;
 constexpr int RS_ABV = RS_GRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
 constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
 #ifndef FLC_RS_STPOL
 #define FLC_RS_STPOL 2                // the dense output's stores: nontemporal (2) or default (0)
+#endif
+#ifndef FLC_RS_GACQ
+#define FLC_RS_GACQ 1                 // k_lone_resident: a group's last arriver acquires before its release
+#endif
+#ifndef FLC_RS_POLLAB
+#define FLC_RS_POLLAB 1               // k_lone_resident: a grid wait reads the abort word every n-th poll
+#endif
+#ifndef FLC_RS_PROBE_NOCOUNT
+#define FLC_RS_PROBE_NOCOUNT 0        // (cost probes only: no exit count — an aborted call would not repair)
+#endif
+#ifndef FLC_RS_G0REL
+#define FLC_RS_G0REL 1                // workgroup 0 releases the row state before it counts out
 #endif
 #ifndef FLC_RS_SPEC
 #define FLC_RS_SPEC 1                 // k_lone_resident: speculative first digit (two digits in one round)
@@ -2388,11 +2403,21 @@ __global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d,
 // prefix is above, +0 elsewhere) and left.  Rows with more elements at that prefix take the third
 // digit and a tie-rank exchange (workgroups publish their tie counts, tagged by the call's sequence
 // number; one holding ties sums those before it).  No sample, no candidate lists, no fallback.
-// The grid must be co-resident: one 1024-thread workgroup per CU, G <= CUs, and the launches are
-// serialised across streams (select.hip host code); a wait past FLC_RS_SPIN ticks of the 100 MHz
-// clock gives up and flags the row (F_OVERFLOW) instead of hanging.  The control block is the
-// library's own, zeroed once; every call leaves it clean (self-resetting barrier counters, replicas
-// cleared by their merger).
+// The grid is meant to be co-resident: one 1024-thread workgroup per CU, G <= CUs, and the
+// launches are serialised across the library's streams (select.hip host code).  Nothing outside
+// the library is: another process's kernels, RCCL's, or a long kernel on a stream of the caller's
+// can hold CUs while the grid starts.  So a wait never trusts stale data.  A wait past `spin`
+// ticks of the 100 MHz clock (FLC_RS_SPIN, 0.1 s) ABORTS the call: it stores the call's sequence
+// number in RS_GAVE, and every workgroup that waits (or later finds the word set) leaves without
+// storing anything; a workgroup only stores output from a completed round, so every store made is
+// a final value.  Every workgroup counts itself out on RS_EXIT (after its last wait, before its
+// stores); the last one out, finding the call aborted, selects the row exactly on its own
+// (rs_repair: three radix passes over the row in HBM and the dense output with the tie ranks, a
+// few ms), rewrites the whole output, puts the control block back to zero and flags the row
+// F_REPAIR.  Correct bits in every case; a clean call pays one counter atomic per workgroup.
+// The control block is the library's own, zeroed once; a clean call leaves it clean
+// (self-resetting barrier counters, replicas cleared by their merger), an aborted one is zeroed by
+// its repair.
 // ------------------------------------------------------------------------------------------
 constexpr int RS_NT = 1024;
 #ifndef FLC_RS_SPIN
@@ -2428,6 +2453,9 @@ __device__ inline bool rs_arrive(const RsTree& tr, uint32_t* flag_s, uint32_t* g
         uint32_t last = 0;
         uint32_t* gc = tr.ctl + RS_GRP + 32 * tr.grp;
         if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tr.gsz - 1u) {
+            // the group's members' writes (released before their arrivals) ordered before this
+            // workgroup's release into the global counter: acquire, then release (transitivity)
+            if (FLC_RS_GACQ) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             if (__hip_atomic_fetch_add(tr.ctl + RS_GLOB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tr.ngr - 1u) {
@@ -2451,24 +2479,113 @@ __device__ inline void rs_release(const RsTree& tr, const uint32_t* gen_s, uint6
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-// everyone else: the release word (thread 0 leaves its payload in res_s[0..1], low word first)
-__device__ inline void rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t* res_s) {
+// everyone else: the release word (thread 0 leaves its payload in res_s[0..1], low word first).
+// false when the call is aborted — this wait passed `spin` ticks (it aborts the call; the first
+// workgroup to abort, *rep_s = 1, repairs it) or another workgroup's did (RS_GAVE holds the
+// call's sequence number): the caller leaves at once.
+__device__ inline bool rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t* res_s, uint32_t* ok_s,
+                               uint32_t* rep_s, uint64_t spin, uint32_t seq) {
     if (threadIdx.x == 0) {
         const uint64_t* rw = reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN);
+        uint32_t* ab = tr.ctl + RS_GAVE;
         const uint64_t t0 = (uint64_t)wall_clock64();
         uint64_t w;
-        while (((uint32_t)(w = __hip_atomic_load(rw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 7u) == *gen_s) {
+        uint32_t ok = 1;
+        for (uint32_t it = 0;; ++it) {
+            // the abort word every FLC_RS_POLLAB-th poll (loaded beside the release word)
+            w = __hip_atomic_load(rw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t a = (it % FLC_RS_POLLAB) == FLC_RS_POLLAB - 1
+                                   ? __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            if (((uint32_t)w & 7u) != *gen_s) break;
+            if (a == seq) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(1);
-            if ((uint64_t)wall_clock64() - t0 > FLC_RS_SPIN) {
-                __hip_atomic_fetch_or(tr.ctl + RS_GAVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint64_t)wall_clock64() - t0 > spin) {
+                if (__hip_atomic_exchange(ab, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) *rep_s = 1;
+                ok = 0;
                 break;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         res_s[0] = (uint32_t)(w >> 3);
         res_s[1] = (uint32_t)(w >> 35);
+        *ok_s = ok;
     }
     __syncthreads();
+    return *ok_s != 0u;
+}
+
+// The repair of an aborted call, by the last workgroup to leave (every other one has gone, none
+// stores anything any more except final values): the control block back to zero, then the row
+// selected exactly on its own — three radix passes (exact_row's 11/11/9-bit digits) over the row
+// in HBM, the elements at the K-th key ranked in index order (tie rule `tie_hi`) — and the whole
+// dense output written: the same function of the row as the resident selection, bit for bit.
+// (32-bit indices: d * 4 < 2^31; the row state words st[0..3] = thr, krem, tiecut, flags.)
+__device__ inline void rs_repair(const float* x, uint32_t d, uint32_t K, uint32_t tie_hi, uint32_t* st_thr,
+                                 uint32_t* st_krem, uint32_t* st_tiecut, uint32_t* st_flags, float* out,
+                                 uint32_t* ctl, uint32_t* h, uint32_t* scratch, uint32_t* wsum) {
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    constexpr uint32_t RU4 = 4;                                        // float4 loads in flight a thread
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < (uint32_t)RS_CTL; i += RS_NT)                 // (RS_EXIT runs on: the host's xbase)
+        if (i != (uint32_t)RS_EXIT) __hip_atomic_store(ctl + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)(d * 4u), 0x00020000);
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(d * 4u), 0x00020000);
+    const uint32_t d4 = (d + 3u) / 4u;
+    uint32_t prefix = 0, krem = K, ties = 0;
+    for (int p = 0; p < 3; ++p) {
+        for (uint32_t i = t; i < (uint32_t)HBINS; i += RS_NT) h[i] = 0;
+        __syncthreads();
+        for (uint32_t f0 = t; f0 < d4; f0 += RU4 * RS_NT) {
+            u4v q[RU4];
+#pragma unroll
+            for (uint32_t u = 0; u < RU4; ++u)                          // past the row: zeros, not counted
+                q[u] = __builtin_amdgcn_raw_buffer_load_b128(rx, (f0 + u * RS_NT) * 16u, 0, 0);
+#pragma unroll
+            for (uint32_t u = 0; u < RU4; ++u)
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t k = q[u][e] & 0x7FFFFFFFu;
+                    if ((f0 + u * RS_NT) * 4u + e < d && key_in_prefix(k, p, prefix)) atomicAdd(&h[key_bin(k, p)], 1u);
+                }
+        }
+        __syncthreads();
+        uint32_t bin, above;
+        hist_find(h, krem, bin, above, scratch);
+        prefix = (prefix << pass_bits(p)) | bin;
+        krem -= above;
+        if (p == 2) ties = h[bin];                                     // the row's keys == the K-th
+        __syncthreads();
+    }
+    const uint32_t thr = prefix;
+    const bool cut = ties > krem;
+    const uint32_t from = tie_hi ? ties - krem : 0u, to = tie_hi ? ties : krem;
+    uint32_t run = 0;                                                  // ties in index order so far
+    for (uint32_t b = 0; b < d4; b += RS_NT) {
+        const uint32_t f = b + t;
+        const u4v q = __builtin_amdgcn_raw_buffer_load_b128(rx, f * 16u, 0, 0);
+        uint32_t ne = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e) ne += (f * 4u + e < d && (q[e] & 0x7FFFFFFFu) == thr) ? 1u : 0u;
+        uint32_t tot;
+        uint32_t r = run + ex_scan<RS_NT>(ne, wsum, tot);
+        u4v o;
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e) {
+            const uint32_t k = q[e] & 0x7FFFFFFFu;
+            const bool eq = f * 4u + e < d && k == thr;
+            const bool keep = k > thr || (eq && (!cut || (r >= from && r < to)));
+            r += eq ? 1u : 0u;
+            o[e] = keep ? q[e] : 0u;
+        }
+        if (f < d4) __builtin_amdgcn_raw_buffer_store_b128(o, ro, f * 16u, 0, 0);   // (range-checked: the row end)
+        run += tot;
+    }
+    if (t == 0) {
+        *st_thr = thr;
+        *st_krem = krem;
+        *st_tiecut = 0;
+        *st_flags = F_RESIDENT | F_REPAIR | (cut ? F_TIES : 0u);
+    }
 }
 
 #ifdef FLC_RS_PRINT                       // probe builds: phase stamps of workgroup 0 (printf)
@@ -2479,11 +2596,11 @@ __device__ inline void rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t
 template <int RU>
 __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d, int64_t K, SelWs ws,
                                                           float* __restrict__ out, int e4, uint32_t* __restrict__ ctl,
-                                                          uint32_t seq) {
+                                                          uint32_t seq, uint64_t spin, uint32_t xbase) {
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
     __shared__ uint32_t wsum[RS_NT / 64];
-    __shared__ uint32_t flag_s, gen_s;
+    __shared__ uint32_t flag_s, gen_s, ok_s;
     const uint32_t G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
 #ifdef FLC_RS_PRINT
     uint64_t stamp[16] = {0};
@@ -2494,6 +2611,30 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     tr.grp = g % RS_NG;
     tr.ngr = min(G, (uint32_t)RS_NG);
     tr.gsz = (G - tr.grp + RS_NG - 1) / RS_NG;
+    // Counted out after the workgroup's last wait and before its stores: one non-returning add to
+    // RS_EXIT (thread 0).  The counter runs over the library's launches on this control block; the
+    // host passes xbase, the workgroups of its earlier launches, so the repairer knows when this
+    // call's others are out (counter - xbase == G - 1) and a clean call needs to know nothing.
+    auto count_out = [&]() {
+        if (t == 0 && !FLC_RS_PROBE_NOCOUNT) __hip_atomic_fetch_add(ctl + RS_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // what an aborted workgroup needs at its exit, stashed in LDS at the start: kept in registers to
+    // the end, these arguments spilled SGPRs all through the dense stores (820 spill slots, not 81)
+    struct RsExit {
+        const float* x;
+        float* out;
+        uint32_t* ctl;
+        uint32_t *thr, *krem, *tiecut, *flags;
+        uint32_t d, K, tie_hi, seq, G, xbase;
+        uint64_t spin;
+    };
+    __shared__ RsExit ex_s;
+    __shared__ uint32_t rep_s;                                          // 1: this workgroup repairs the call
+    if (t == 0) {
+        rep_s = 0;
+        ex_s = RsExit{rows.row_s(0), out, ctl, ws.thr, ws.krem, ws.tiecut, ws.flags, (uint32_t)d, (uint32_t)K, ws.tie_hi, seq,
+                      G, xbase, spin};
+    }
     const uint32_t nb = (uint32_t)(d * 4);                               // d <= RS_U * 4096 * CUs
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(0)), (short)0, (int)nb, 0x00020000);
     const auto ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)nb, 0x00020000);
@@ -2637,7 +2778,7 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 __hip_atomic_store(s0 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             RS_STAMP(2);
-            rs_wait(tr, &gen_s, scratch);
+            if (!rs_wait(tr, &gen_s, scratch, &ok_s, &rep_s, spin, seq)) goto leave;
         }
         __syncthreads();
         const uint64_t pl = ((uint64_t)scratch[1] << 32) | scratch[0];
@@ -2705,7 +2846,7 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 for (int r = 0; r < RS_NG; ++r) __hip_atomic_store(r0 + r * HBINS + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             RS_STAMP(2 + 3 * p);
-            rs_wait(tr, &gen_s, scratch);
+            if (!rs_wait(tr, &gen_s, scratch, &ok_s, &rep_s, spin, seq)) goto leave;
         }
         __syncthreads();
         const uint64_t pl = ((uint64_t)scratch[1] << 32) | scratch[0];
@@ -2789,32 +2930,33 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         RS_STAMP(10);
         if (rs_arrive(tr, &flag_s, &gen_s, 0u)) {
             // the last workgroup: rank the m listed elements, store the krem first and +0 for the
-            // rest (then its own dense output)
+            // rest (then its own dense output).  Every workgroup arrived here, so no wait of the
+            // call gave up and none is left; a list that does not add up (never seen) aborts the
+            // call instead of storing anything doubtful, and the repair selects the row.
             __shared__ uint64_t comp[RS_CAP];
             __shared__ uint64_t kth_s;
             const uint32_t m = __hip_atomic_load(ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool ok = m == last && m >= krem && krem >= 1u;          // every element at P listed
-            const uint32_t mm = min(m, (uint32_t)RS_CAP);
+            const bool ok = m == last && m >= krem && krem >= 1u && m <= (uint32_t)RS_CAP;   // every element at P listed
+            const uint32_t mm = ok ? m : 0u;
             for (uint32_t i = t; i < mm; i += RS_NT) {
                 const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 comp[i] = ((uint64_t)((uint32_t)(en >> 32) & 0x7FFFFFFFu) << 32) | tie_pref((uint32_t)en, ws.tie_hi);
             }
             if (t == 0) { scratch[2] = 0; scratch[3] = 0; kth_s = ~0ull; }
             __syncthreads();
-            if (ok)
-                for (uint32_t i = t; i < mm; i += RS_NT) {
-                    const uint64_t me = comp[i];
-                    uint32_t rank = 0;
-                    for (uint32_t jj = 0; jj < mm; ++jj) rank += comp[jj] > me ? 1u : 0u;
-                    if (rank == krem - 1u) kth_s = me;                   // entries are distinct
-                }
+            for (uint32_t i = t; i < mm; i += RS_NT) {
+                const uint64_t me = comp[i];
+                uint32_t rank = 0;
+                for (uint32_t jj = 0; jj < mm; ++jj) rank += comp[jj] > me ? 1u : 0u;
+                if (rank == krem - 1u) kth_s = me;                       // entries are distinct
+            }
             __syncthreads();
             const uint64_t kc = kth_s;
             const uint32_t kth = (uint32_t)(kc >> 32);
             for (uint32_t i = t; i < mm; i += RS_NT) {
                 const uint64_t me = comp[i];
                 const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                out[(uint32_t)en] = (ok && me >= kc) ? __uint_as_float((uint32_t)(en >> 32)) : 0.f;
+                out[(uint32_t)en] = me >= kc ? __uint_as_float((uint32_t)(en >> 32)) : 0.f;
                 const uint32_t key = (uint32_t)(me >> 32);
                 if (key > kth) atomicAdd(&scratch[2], 1u);
                 else if (key == kth) atomicAdd(&scratch[3], 1u);
@@ -2823,14 +2965,18 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             if (t == 0) {
                 __hip_atomic_store(ctl + RS_CCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // clean for the next call
                 const uint32_t gt = scratch[2], eq = scratch[3];
-                const bool gave_up = __hip_atomic_exchange(ctl + RS_GAVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
                 ws.thr[0] = kth;
                 ws.krem[0] = krem - gt;
                 ws.tiecut[0] = tie_pref((uint32_t)kc, ws.tie_hi);
-                ws.flags[0] = F_RESIDENT | (gt + eq > krem ? F_TIES : 0u) | ((gave_up || !ok) ? F_OVERFLOW : 0u);
+                ws.flags[0] = F_RESIDENT | (gt + eq > krem ? F_TIES : 0u);
+                if (!ok && __hip_atomic_exchange(ctl + RS_GAVE, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq)
+                    rep_s = 1;
             }
+            if (!ok) goto leave;                                         // (uniform) aborted: repaired
+            count_out();
             dense();
         } else {
+            count_out();
             dense();
         }
         RS_STAMP(11);
@@ -2860,18 +3006,26 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         if (t == 0) __hip_atomic_store(tc + g, ((uint64_t)seq << 32) | tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         if (tot == 0u) goto store;                                       // (uniform) no tie here
         uint32_t part = 0, run = 0;
-        for (uint32_t i = t; i < g; i += RS_NT) {
-            const uint64_t t0 = (uint64_t)wall_clock64();
+        int bail = 0;
+        const uint64_t t0 = (uint64_t)wall_clock64();
+        for (uint32_t i = t; i < g && !bail; i += RS_NT) {
             uint64_t w;
-            while ((uint32_t)((w = __hip_atomic_load(tc + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != seq) {
+            for (;;) {
+                w = __hip_atomic_load(tc + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t a = __hip_atomic_load(ctl + RS_GAVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(w >> 32) == seq) break;
+                if (a == seq) { bail = 1; break; }                       // aborted elsewhere
                 __builtin_amdgcn_s_sleep(1);
-                if ((uint64_t)wall_clock64() - t0 > FLC_RS_SPIN) {
-                    __hip_atomic_fetch_or(ctl + RS_GAVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint64_t)wall_clock64() - t0 > spin) {             // a workgroup before is not running
+                    if (__hip_atomic_exchange(ctl + RS_GAVE, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq)
+                        rep_s = 1;                                       // (one thread of the grid)
+                    bail = 1;
                     break;
                 }
             }
             part += (uint32_t)w;
         }
+        if (__syncthreads_or(bail)) goto leave;                          // (uniform) the call is aborted
         (void)ex_scan<RS_NT>(part, wsum, run);                           // ties in the workgroups before
         const uint32_t tie_from = ws.tie_hi ? last - krem : 0u, tie_to = ws.tie_hi ? last : krem;
 #pragma unroll
@@ -2895,6 +3049,17 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     }
 store:
     RS_STAMP(10);
+    // every wait of this workgroup is behind it: the row state (workgroup 0: released before it is
+    // counted out, so that a repair's later state is the one that stays), counted out, then the
+    // stores (final values)
+    if (g == 0 && t == 0) {
+        ws.thr[0] = thr;
+        ws.krem[0] = krem;
+        ws.tiecut[0] = 0;
+        ws.flags[0] = F_RESIDENT | (tie_cut ? F_TIES : 0u);
+        if (FLC_RS_G0REL) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    count_out();
     // the dense output from the registers: x where kept, +0 elsewhere (range-checked: no padding)
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
@@ -2912,17 +3077,40 @@ store:
         }
     }
     RS_STAMP(11);
-    // row state for flc_select_row_flags (every workgroup knows it; workgroup 0 writes it)
-    if (g == 0 && t == 0) {
-        // (a wait that gave up: flagged; the flag is cleared for the next call's report)
-        const bool gave_up = __hip_atomic_exchange(ctl + RS_GAVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        (void)bar;
-        ws.thr[0] = thr;
-        ws.krem[0] = krem;
-        ws.tiecut[0] = 0;
-        ws.flags[0] = F_RESIDENT | (tie_cut ? F_TIES : 0u) | (gave_up ? F_OVERFLOW : 0u);
+    (void)bar;
     }
+    goto done;
+leave:
+    // An aborted workgroup (it left from a wait, or the ranking found the list inconsistent): its
+    // control-block writes completed (release), then counted out — except the repairer (the first
+    // to abort), which waits for every other workgroup of the call to be out, selects the row on
+    // its own, rewrites the output and the row state, zeroes the control block, then counts out.
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (!rep_s) __hip_atomic_fetch_add(ex_s.ctl + RS_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __syncthreads();
+    if (rep_s) {
+        const RsExit ex = ex_s;
+        if (t == 0) {
+            // (bounded: every other workgroup leaves within its own waits' limit once it runs; a
+            // grid that cannot drain at all after 64 of them is repaired anyway — its stragglers
+            // never store anything but final values)
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            while ((uint32_t)(__hip_atomic_load(ex.ctl + RS_EXIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ex.xbase) < ex.G - 1u &&
+                   (uint64_t)wall_clock64() - t0 < 64 * ex.spin)
+                __builtin_amdgcn_s_sleep(8);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        __syncthreads();
+        rs_repair(ex.x, ex.d, ex.K, ex.tie_hi, ex.thr, ex.krem, ex.tiecut, ex.flags, ex.out, ex.ctl, h, scratch, wsum);
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_fetch_add(ex.ctl + RS_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+done:
 #ifdef FLC_RS_PRINT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -3054,11 +3242,22 @@ static bool cs_single() {            // tuning runs: FLC_CS_SINGLE=1 keeps the o
 struct RsCtx {
     uint32_t* ctl = nullptr;
     uint32_t seq = 0;                   // launches so far (tags the tie counts of each call)
+    uint32_t xcum = 0;                  // workgroups launched so far (RS_EXIT's count before a launch)
     hipStream_t last = nullptr;
     hipEvent_t done = nullptr;
 };
 static std::mutex g_rs_mu;
 static std::map<int, RsCtx> g_rs_ctx;
+// test hook (flc_debug_resident): the grid of the next resident launches x mult (workgroups that
+// cannot all be resident: the abort + repair path, deterministically) and the waits' give-up time
+static std::atomic<int> g_rs_dbg_mult{1};
+static std::atomic<long long> g_rs_dbg_spin{0};
+int rs_debug(int mult, int64_t spin_ticks) {
+    if (mult < 1 || mult > 64 || spin_ticks < 0) { set_error("flc_debug_resident: mult 1..64, spin >= 0"); return FLC_ERR_ARG; }
+    g_rs_dbg_mult.store(mult);
+    g_rs_dbg_spin.store((long long)spin_ticks);
+    return FLC_OK;
+}
 static int rs_cus() {              // compute units of the current device (one k_lone_resident workgroup each)
     static int cu[64] = {0};
     int dev = 0;
@@ -3328,13 +3527,20 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
             FLC_CHECK_LAUNCH("k_randk_fine");
         }
     } else {  // TOPK
-        // a lone compressVector row up to RS_U * 4096 elements per CU (any K): in registers, one launch
-        if (assign && n == 1 && !assign_fold() && lone_path() == 2) {
+        // a lone compressVector row up to RS_U * 4096 elements per CU (any K): in registers, one
+        // launch.  Not inside a stream capture (the call's sequence number and the cross-stream
+        // serialisation are host state a replayed graph would not redo): the list path there.
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (assign && n == 1 && !assign_fold() && lone_path() == 2) FLC_CHECK_HIP(hipStreamIsCapturing(st, &cap));
+        if (assign && n == 1 && !assign_fold() && lone_path() == 2 && cap == hipStreamCaptureStatusNone) {
             const int64_t cus = rs_cus();
-            const int64_t G = std::min<int64_t>(cus, (d + RS_NT * 4 - 1) / (RS_NT * 4));
+            const int mult = std::max(1, g_rs_dbg_mult.load());              // (test hook: > 1 forces an aborted call)
+            const int64_t G = std::min<int64_t>(cus * mult, (d + RS_NT * 4 - 1) / (RS_NT * 4));
             const int64_t e4 = G > 0 ? (d + G * RS_NT * 4 - 1) / (G * RS_NT * 4) : RS_U + 1;
             if (e4 <= RS_U && d * 4 < ((int64_t)1 << 31)) {
                 const int64_t Gu = (d + e4 * RS_NT * 4 - 1) / (e4 * RS_NT * 4);   // no workgroup of padding only
+                const long long dspin = g_rs_dbg_spin.load();
+                const uint64_t spin = dspin > 0 ? (uint64_t)dspin : (uint64_t)FLC_RS_SPIN;
                 ProfScope _ps("k_lone_resident", st);
                 int dev = 0;
                 FLC_CHECK_HIP(hipGetDevice(&dev));
@@ -3342,15 +3548,14 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                 RsCtx& rc = g_rs_ctx[dev];
                 if (!rc.ctl) {
                     FLC_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&rc.ctl), (size_t)RS_CTL * sizeof(uint32_t)));
-                    FLC_CHECK_HIP(hipMemset(rc.ctl, 0, (size_t)RS_CTL * sizeof(uint32_t)));
+                    FLC_CHECK_HIP(hipMemsetAsync(rc.ctl, 0, (size_t)RS_CTL * sizeof(uint32_t), st));
                     FLC_CHECK_HIP(hipEventCreateWithFlags(&rc.done, FLC_SYNC_EVENT_FLAGS));
                 }
-                hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-                FLC_CHECK_HIP(hipStreamIsCapturing(st, &cap));
-                if (rc.last && rc.last != st && cap == hipStreamCaptureStatusNone) {
+                if (rc.last && rc.last != st) {
                     if (!FLC_RS_EVREC) FLC_CHECK_HIP(hipEventRecord(rc.done, rc.last));   // (probe builds)
                     FLC_CHECK_HIP(hipStreamWaitEvent(st, rc.done, 0));
                 }
+                if (++rc.seq == 0u) rc.seq = 1u;                              // (0: no call; RS_GAVE's cleared value)
                 const int e4i = (int)e4;
                 if (FLC_RS_COOP) {
                     RowSrc ra = rows;
@@ -3359,18 +3564,20 @@ int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bo
                     float* oa = out;
                     int ea = e4i;
                     uint32_t* ca = rc.ctl;
-                    uint32_t sa = ++rc.seq;
-                    void* args[] = {&ra, &da, &ka, &wa, &oa, &ea, &ca, &sa};
+                    uint32_t sa = rc.seq;
+                    uint64_t pa = spin;
+                    uint32_t xa = rc.xcum;
+                    void* args[] = {&ra, &da, &ka, &wa, &oa, &ea, &ca, &sa, &pa, &xa};
                     FLC_CHECK_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_lone_resident<RS_U>), dim3((unsigned)Gu),
                                                              dim3(RS_NT), args, 0, st));
                 } else {
-                    hipLaunchKernelGGL((k_lone_resident<RS_U>), dim3((unsigned)Gu), dim3(RS_NT), 0, st, rows, d, K, ws, out, e4i, rc.ctl, ++rc.seq);
-                }
-                if (cap == hipStreamCaptureStatusNone) {
-                    if (FLC_RS_EVREC) FLC_CHECK_HIP(hipEventRecord(rc.done, st));
-                    rc.last = st;
+                    hipLaunchKernelGGL((k_lone_resident<RS_U>), dim3((unsigned)Gu), dim3(RS_NT), 0, st, rows, d, K, ws, out, e4i,
+                                       rc.ctl, rc.seq, spin, rc.xcum);
                 }
                 FLC_CHECK_LAUNCH("k_lone_resident");
+                rc.xcum += (uint32_t)Gu;                                      // (every workgroup counts out once)
+                if (FLC_RS_EVREC) FLC_CHECK_HIP(hipEventRecord(rc.done, st));
+                rc.last = st;
                 return FLC_OK;
             }
         }

@@ -292,11 +292,15 @@ int flc_device_randk_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d
 
 /* The fp32 2-norm of each of n rows (row i at d_rows + i*ld) in torch's CPU reduction order —
  * the norm the reference computes, compressors.py:272 `torch.norm(x, p=2)` on a CPU fp32
- * tensor, bit for bit (torch 2.10: 8 lane accumulators of fused multiply-adds summed left to
- * right, the D % 8 tail added in order, then the correctly rounded sqrt; oracle/torch_norm.c,
- * pinned by tests/golden/rows.json at D = 25 M).  Not exactly rounded (14 616 ulp below the exact
- * norm at D = 25 M); hand it to flc_encode's d_pnorm_in to get the reference's dithering bits.
- * Each row is D / 8 dependent fmas per lane: latency-bound (a parity mode, ~ms at D = 25 M). */
+ * tensor, bit for bit ON AN x86 HOST WITH AVX2 (torch 2.10's AVX2 Vectorized<float> of 8 lanes —
+ * the norm kernel has no AVX512 registration, so AVX512 hosts run it too: 8 lane accumulators of
+ * fused multiply-adds summed left to right, the D % 8 tail added in order, then the correctly
+ * rounded sqrt; oracle/torch_norm.c, pinned by tests/golden/rows.json at D = 25 M and against
+ * torch on an AVX512 host by tests/test_host.py).  A torch without AVX2 kernels (DEFAULT
+ * capability, non-x86) sums in another lane count: parity there is unpinned.  Not exactly rounded (14 616 ulp below
+ * the exact norm at D = 25 M); hand it to flc_encode's d_pnorm_in to get the reference's dithering
+ * bits (standard and natural dithering, compressors.py:272 / 303).  Each row is D / 8 dependent
+ * fmas per lane: latency-bound (a parity mode; bench.py --dropin --norm-mode torch_cpu prices it). */
 int flc_norm2_torch_cpu(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* stream);
 
 /* Self-test of the exact fast fp32 division the dithering kernels use: for each of the n
@@ -322,11 +326,20 @@ int flc_profile_collect(const char* kernel, double* h_total_ms, int64_t* h_launc
  * overflowed, 2 it came up short, 4 ambiguous ties at the K-th key resolved on the fast path,
  * 8 the row was selected by the exact path (the fast path failed — bits 1 / 2 then say why — or
  * K > D/16), 16 a lone compressVector row (flc_encode, n = 1) selected exactly in registers in one
- * launch (rows up to 16 float4 x 4096 x the device's CUs; 4 then marks a tie cut, 1 a grid wait
- * that gave up).  Rows that stayed on the fast path read 0 or 4.  (Replaces nothing in the
- * reference: compressors.py:330-335 has one path.) */
+ * launch (rows up to 16 float4 x 4096 x the device's CUs; 4 then marks a tie cut), 32 (with 16)
+ * that launch's grid was not co-resident — a grid wait gave up, the call was aborted and its last
+ * workgroup re-selected the row exactly (same result).  Rows that stayed on the fast path read 0
+ * or 4.  (Replaces nothing in the reference: compressors.py:330-335 has one path.) */
 int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* d_workspace,
                          size_t ws_bytes, uint32_t* d_flags, void* stream);
+
+/* Test hook of the lone-TopK resident selection (no compute): the next resident launches of this
+ * process use grid_mult x their grid (grid_mult > 1: more 1024-thread workgroups than can be
+ * resident at once, so the call's grid waits give up and its abort + exact repair path runs) and
+ * give up a grid wait after spin_ticks of the 100 MHz clock (0: the default, 0.1 s).
+ * flc_debug_resident(1, 0) restores the defaults.  FLC_ERR_ARG outside grid_mult 1..64,
+ * spin_ticks >= 0.  (Replaces nothing in the reference.) */
+int flc_debug_resident(int grid_mult, int64_t spin_ticks);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,9 @@
  * sqrtf.  Determined empirically against torch.norm in the development container (69 of 69
  * random vectors, D from 1 to 1 000 003, mixed magnitudes; tests/test_host.py) and pinned by
  * the reference's own norms at D = 25 M (tests/golden/rows.json pnorm_bits).
+ * ASSUMPTION: torch's AVX2 (8-lane) norm kernel, which x86 hosts with AVX2 run — AVX512
+ * hosts too, the kernel has no AVX512 registration (this container's torch reports AVX512 and
+ * matches; tests/test_host.py).  A torch without AVX2 kernels is unpinned.
  * Every operation is fp32 with one rounding (fmaf): the C compiler must not contract or
  * reassociate (-ffp-contract=off, no -ffast-math).
  */

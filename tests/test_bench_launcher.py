@@ -77,3 +77,33 @@ def test_dist_info_fields_over_gloo(tmp_path):
     assert [r["rank"] for r in info["ranks"]] == [0, 1]
     assert info["allreduce_bytes"] == 4000 and info["allreduce_ms"] > 0 and info["allreduce_busbw_GBps"] > 0
     assert info["distinct_devices"] == 1          # CPU tensors: no device to tell the ranks apart
+
+
+_STRONG_CODE = (
+    "import json, sys, torch, torch.distributed as dist; sys.path.insert(0, r'%s'); import bench;"
+    "dist.init_process_group('gloo');"
+    "d = 1000; rows = torch.from_numpy(__import__('numpy').random.default_rng(3).standard_normal((4, d)).astype('float32'));"
+    # a toy encode whose partial depends on the client ids (as the device-RNG draws do)
+    "enc = lambda r, c0, out: out.copy_(sum(r[i] * float(1 + (c0 + i) %% 7) for i in range(r.shape[0])));"
+    "fold = lambda st, tot: (lambda a: [a.add_(st[b]) for b in range(1, st.shape[0])] and a.div_(torch.tensor(float(tot))))(st[0].clone());"
+    "b = bench.strong_block(enc, fold, rows, 32, d, torch.device('cpu'), steps=2, warmup=1, group=dist.group.WORLD);"
+    "(open(r'%s', 'w').write(json.dumps(b)) if dist.get_rank() == 0 else None);"
+    "dist.destroy_process_group()")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_strong_block_digest_is_g_invariant(tmp_path, world):
+    """bench.strong_block (the strong_c4 block of every default line) over gloo
+    with CPU tensors: 32 clients in 8 fixed blocks of 4 resident rows replayed per block with the
+    block's client ids, the ordered combine — the result digest at G = world equals G = 1's, and
+    the block reports G, the clients per rank, the step time and the whole-job rate."""
+    outs = {}
+    for g in (1, world):
+        out = tmp_path / f"strong{g}.json"
+        assert bench.launch_ranks(g, [sys.executable, "-c", _STRONG_CODE % (ROOT, out)]) == 0
+        outs[g] = json.loads(out.read_text())
+    assert outs[1]["result_sha256"] == outs[world]["result_sha256"]
+    assert outs[1]["n_gpus"] == 1 and outs[world]["n_gpus"] == world
+    assert outs[1]["clients_per_gpu"] == 32 and outs[world]["clients_per_gpu"] == 32 // world
+    for b in outs.values():
+        assert b["ms_per_step"] > 0 and b["value_GBps"] > 0 and b["clients_total"] == 32

@@ -81,3 +81,32 @@ def test_compressvector_norm_mode_torch_cpu():
     want = o.compress(x, pnorm=oracle_norm(x))
     got = c.compressVector(torch.from_numpy(x).cuda()).cpu().numpy()
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("spec", ["nat.dithering:4:2", "nat.dithering:8:2", "std.dithering:16:2"])
+def test_compressvector_norm_mode_torch_cpu_dithering_p2(spec):
+    """natural dithering (compressors.py:301-329) takes torch.norm(x, p) as well and
+    its output y * sign * pnorm carries the norm's bits, so norm_mode='torch_cpu' applies to it (p = 2)
+    like to standard dithering: bit-exact against the oracle given the torch-order norm; and the
+    natural dithering output differs from the exact-norm one exactly where the norms differ."""
+    from flpytorch_amd import aggregation as ag
+    from oracle import codecs as oc
+    from oracle.rng import OracleRandomState
+    d = 200_003
+    x = np.random.default_rng(len(spec)).standard_normal(d).astype(np.float32)
+    c = ag.initCompressor(spec, d)
+    c.norm_mode = "torch_cpu"
+    c.generateCompressPattern(np.random.RandomState(4), "cuda", 0, None)
+    o = oc.OracleCompressor(spec, d)
+    o.generate(OracleRandomState(4))
+    want = o.compress(x, pnorm=oracle_norm(x))
+    got = c.compressVector(torch.from_numpy(x).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_norm_mode_torch_cpu_p1_not_restated():
+    from flpytorch_amd import aggregation as ag
+    c = ag.initCompressor("nat.dithering:4:1", 1000)
+    c.norm_mode = "torch_cpu"
+    with pytest.raises(NotImplementedError):
+        c.compressVector(torch.ones(1000, device="cuda"))

@@ -210,3 +210,86 @@ def test_compressvector_resident_speculation_miss(ag, where):
         np.testing.assert_array_equal(_bits(c.compressVector(xt)), _bits(_enc([x], k, tie)[0]), err_msg=tie)
         f = int(ag.select_row_flags(c, 1, d)[0])
         assert f & 16 and not f & 1, f"{tie}: flags {f}"
+
+
+def _debug_resident(mult, spin_ticks):
+    from flpytorch_amd import _lib
+    _lib.check(_lib.load().flc_debug_resident(mult, spin_ticks), "flc_debug_resident")
+
+
+@pytest.mark.parametrize("d,kind", [(4_000_003, "normal"), (4_000_003, "ties"), (10_000_000, "normal"),
+                                    (2_100_001, "fewnz"), (10_000_000, "ties")])
+def test_compressvector_resident_not_coresident(ag, d, kind):
+    """k_lone_resident's grid barrier assumes its workgroups are all resident; other kernels (another
+    process, RCCL, a long kernel on a caller's stream) can hold CUs.  Forced
+    here deterministically: flc_debug_resident(2, 1 ms) launches twice the grid (2 x CUs 1024-thread
+    workgroups, one fits a CU), so the resident half waits for workgroups that cannot start, its
+    waits give up after 1 ms and abort the call, and the last workgroup out re-selects the row
+    exactly (F_REPAIR, 32).  The output must be the oracle's bits under both tie rules — never a
+    silent wrong result — and the next call (the control block back to zero) clean and exact."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    g = np.random.default_rng([d, len(kind), 5])
+    k = max(1, d // 100)
+    x = g.standard_normal(d).astype(np.float32)
+    if kind == "fewnz":
+        x[np.argsort(g.random(d))[: d - k // 3]] = 0.0
+    elif kind == "ties":
+        x = _straddle(x[None, :].copy(), k, g, places=(3,), nties=(400,))[0]
+    xt = torch.from_numpy(x).cuda()
+    g2 = min(2 * cus, -(-d // 4096))
+    e4 = -(-d // (g2 * 4096))
+    gu = -(-d // (e4 * 4096))                                     # the forced grid (select.hip host code)
+    for tie in ("lowest", "highest"):
+        want = _bits(_enc([x], k, tie)[0])
+        c = _comp(ag, f"topk:{k}", d, tie)
+        _debug_resident(2, 100_000)
+        try:
+            got = c.compressVector(xt)
+            torch.cuda.synchronize()
+        finally:
+            _debug_resident(1, 0)
+        np.testing.assert_array_equal(_bits(got), want, err_msg=f"{tie}: forced non-resident grid")
+        f = int(ag.select_row_flags(c, 1, d)[0])
+        if gu > cus:
+            assert f & 16 and f & 32, f"{tie}: flags {f}, expected the repaired resident call ({gu} workgroups, {cus} CUs)"
+        # the next call on the default grid: the control block was left clean
+        got2 = c.compressVector(xt)
+        np.testing.assert_array_equal(_bits(got2), want, err_msg=f"{tie}: the call after a repaired one")
+        f2 = int(ag.select_row_flags(c, 1, d)[0])
+        assert f2 & 16 and not f2 & 32, f"{tie}: flags {f2} after the repair"
+
+
+def test_debug_resident_validation(ag):
+    from flpytorch_amd import _lib
+    lib = _lib.load()
+    assert lib.flc_debug_resident(0, 0) != 0
+    assert lib.flc_debug_resident(2, -1) != 0
+    assert lib.flc_debug_resident(1, 0) == 0
+
+
+def test_compressvector_under_graph_capture(ag):
+    """inside a stream capture a lone TopK compressVector must not use the
+    register-resident launch (its call sequence number and cross-stream serialisation are host state
+    a replayed graph would not redo): the captured graph runs the list path and every replay gives
+    the oracle's bits, also on rows with ties at the K-th key."""
+    d, k = 2_000_003, 20_000
+    g = np.random.default_rng(41)
+    x = _straddle(g.standard_normal(d).astype(np.float32)[None, :].copy(), k, g, places=(2,), nties=(9,))[0]
+    xt = torch.from_numpy(x).cuda()
+    c = _comp(ag, f"topk:{k}", d, "lowest")
+    want = _bits(_enc([x], k, "lowest")[0])
+    np.testing.assert_array_equal(_bits(c.compressVector(xt)), want)        # warm: workspace, level tables
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        np.testing.assert_array_equal(_bits(c.compressVector(xt)), want)    # the capture stream's workspace
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        out = c.compressVector(xt)
+    for _ in range(3):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_bits(out), want)

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.flc_version() == _lib.ABI_VERSION == 101
+    assert lib.flc_version() == _lib.ABI_VERSION == 102
 
 
 def test_library_build_id_matches_tree():
@@ -370,6 +370,12 @@ def test_torch_norm_oracle_vs_torch_on_this_host():
     import torch
 
     from oracle import rng
+    # the restatement's 8 lanes are torch's AVX2 Vectorized<float>.  The norm kernel has
+    # no AVX512 registration, so an AVX512 host (this container reports "AVX512") runs the same AVX2
+    # kernel — this test pins that; a torch without AVX2 ("DEFAULT", non-x86) is unpinned
+    cap = torch.backends.cpu.get_cpu_capability()
+    if cap not in ("AVX2", "AVX512"):
+        pytest.skip(f"torch's {cap} CPU kernels: the 8-lane (AVX2) restatement is unpinned here")
     rng._load()
     lib = ctypes.CDLL(rng._LIB_PATH)
     lib.orc_torch_norm2.restype = ctypes.c_float

@@ -63,7 +63,19 @@ def main():
     fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch", kernel)
     write, nw = run_pass("WRITE_SIZE", a.workload, extra, base + "_write", kernel)
     launches = max(nf, nw, 1)
+    # what the counters were taken on, so that bench.py attaches them only to a line of the same
+    # shape: rows per GPU, D, the dominant kernel's launches per step (the bench
+    # runs warmup + the timed steps + the same steps again for the kernel events; a drop-in run
+    # launches its kernel once per compressVector)
+    sys.path.insert(0, ROOT)
+    import bench
+    wl = bench.WORKLOADS[a.workload]
+    n_rows = a.n or (8 if a.dropin else wl["n"])
+    runs = 1 + 2 * a.steps
     res = {"workload": a.workload, "kernel": kernel, "n_override": a.n, "compat": bool(a.compat), "dropin": bool(a.dropin),
+           "n": n_rows, "d": wl["d"], "steps": a.steps, "warmup": 1,
+           "launches_per_step": None if a.dropin else round(launches / runs, 3),
+           "rows_per_launch": 1 if a.dropin else round(n_rows * runs / launches, 3),
            "launches": launches, "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024 / launches),
            "correction": "2 x FETCH_SIZE (gfx950 tallies each 128-B line request at 64 B: every streamed "
