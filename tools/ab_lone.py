@@ -53,7 +53,8 @@ def main():
 
     res = {v: [] for v in variants}
     for r in range(a.rounds):
-        for v in variants:
+        # the variants' order reversed every other round: no variant always runs first / after another
+        for v in (variants if r % 2 == 0 else variants[::-1]):
             with _lib.use(libs[v]):
                 outs = run_all()                                   # warm + output for the bit check
                 torch.cuda.synchronize()

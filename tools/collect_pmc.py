@@ -57,7 +57,7 @@ def main():
     kernel = a.kernel or (DROPIN_KERNEL if a.dropin else KERNEL_SUBSTR)[a.workload]
     tag = a.tag or (("dropin_" if a.dropin else "") + a.workload + ("_compat" if a.compat else ""))
     extra = ["--steps", str(a.steps), "--warmup", "1"] + (["--n", str(a.n)] if a.n else []) + (["--compat"] if a.compat else [])
-    extra += ["--dropin"] if a.dropin else ["--no-cpu-baseline"]
+    extra += ["--dropin"] if a.dropin else ["--no-cpu-baseline", "--no-strong-c4"]
     os.environ.setdefault("TMPDIR", "/tmp")
     base = os.path.join(ROOT, "gpurun_out", f"pmc_traffic_{tag}")
     fetch, nf = run_pass("FETCH_SIZE", a.workload, extra, base + "_fetch", kernel)
