@@ -58,9 +58,10 @@ constexpr int RS_NG = FLC_RS_NG;
 constexpr int RS_NG_MAX = 16;
 static_assert(RS_NG >= 1 && RS_NG <= RS_NG_MAX, "FLC_RS_NG: 1..16 groups");
 // its control words: counters on lines of their own, per-group digit histograms, tie counts
-// (RS_GAVE: the sequence number of a call that was aborted; RS_EXIT: workgroups that have left)
-constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_EXIT = 128, RS_GRP = 160;
-constexpr int RS_ABV = RS_GRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
+// (RS_GAVE: the sequence number of a call that was aborted; RS_XGRP: workgroups that have left)
+constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128;
+constexpr int RS_XGRP = RS_GRP + 32 * RS_NG_MAX;  // per group: workgroups counted out (runs on across calls)
+constexpr int RS_ABV = RS_XGRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
 constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
 #ifndef FLC_RS_STPOL
@@ -2410,11 +2411,13 @@ __global__ __launch_bounds__(EX_NT) void k_assign_finish(RowSrc rows, int64_t d,
 // ticks of the 100 MHz clock (FLC_RS_SPIN, 0.1 s) ABORTS the call: it stores the call's sequence
 // number in RS_GAVE, and every workgroup that waits (or later finds the word set) leaves without
 // storing anything; a workgroup only stores output from a completed round, so every store made is
-// a final value.  Every workgroup counts itself out on RS_EXIT (after its last wait, before its
-// stores); the last one out, finding the call aborted, selects the row exactly on its own
-// (rs_repair: three radix passes over the row in HBM and the dense output with the tie ranks, a
-// few ms), rewrites the whole output, puts the control block back to zero and flags the row
-// F_REPAIR.  Correct bits in every case; a clean call pays one counter atomic per workgroup.
+// a final value.  Every workgroup counts itself out on its group's RS_XGRP counter (after its last
+// wait, before its stores; counters that run on across calls, the host passing the count before
+// the launch).  The FIRST workgroup to abort instead waits for all the others to be out, then
+// selects the row exactly on its own (rs_repair: three radix passes over the row in HBM and the
+// dense output with the tie ranks, a few ms), rewrites the whole output, puts the control block
+// back to zero and flags the row F_REPAIR.  Correct bits in every case; a clean call pays one
+// non-returning counter atomic per workgroup.
 // The control block is the library's own, zeroed once; a clean call leaves it clean
 // (self-resetting barrier counters, replicas cleared by their merger), an aborted one is zeroed by
 // its repair.
@@ -2526,8 +2529,9 @@ __device__ inline void rs_repair(const float* x, uint32_t d, uint32_t K, uint32_
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     constexpr uint32_t RU4 = 4;                                        // float4 loads in flight a thread
     const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < (uint32_t)RS_CTL; i += RS_NT)                 // (RS_EXIT runs on: the host's xbase)
-        if (i != (uint32_t)RS_EXIT) __hip_atomic_store(ctl + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = t; i < (uint32_t)RS_CTL; i += RS_NT)                 // (RS_XGRP runs on: the host's xbase)
+        if (i < (uint32_t)RS_XGRP || i >= (uint32_t)(RS_XGRP + 32 * RS_NG_MAX))
+            __hip_atomic_store(ctl + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)(d * 4u), 0x00020000);
     const auto ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(d * 4u), 0x00020000);
     const uint32_t d4 = (d + 3u) / 4u;
@@ -2612,11 +2616,14 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     tr.ngr = min(G, (uint32_t)RS_NG);
     tr.gsz = (G - tr.grp + RS_NG - 1) / RS_NG;
     // Counted out after the workgroup's last wait and before its stores: one non-returning add to
-    // RS_EXIT (thread 0).  The counter runs over the library's launches on this control block; the
-    // host passes xbase, the workgroups of its earlier launches, so the repairer knows when this
-    // call's others are out (counter - xbase == G - 1) and a clean call needs to know nothing.
+    // its group's RS_XGRP counter (thread 0; one counter for the grid serialised ~245 atomics on one
+    // address and held the kernel's end ~1 us).  The counters run over the library's launches on
+    // this control block; the host passes xbase, the workgroups of its earlier launches, so the
+    // repairer knows when this call's others are out (sum - xbase == G - 1) and a clean call needs
+    // to know nothing.
     auto count_out = [&]() {
-        if (t == 0 && !FLC_RS_PROBE_NOCOUNT) __hip_atomic_fetch_add(ctl + RS_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 && !FLC_RS_PROBE_NOCOUNT)
+            __hip_atomic_fetch_add(ctl + RS_XGRP + 32 * tr.grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // what an aborted workgroup needs at its exit, stashed in LDS at the start: kept in registers to
     // the end, these arguments spilled SGPRs all through the dense stores (820 spill slots, not 81)
@@ -3087,8 +3094,8 @@ leave:
     // its own, rewrites the output and the row state, zeroes the control block, then counts out.
     if (t == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (!rep_s) __hip_atomic_fetch_add(ex_s.ctl + RS_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (!rep_s) count_out();
     __syncthreads();
     if (rep_s) {
         const RsExit ex = ex_s;
@@ -3097,18 +3104,20 @@ leave:
             // grid that cannot drain at all after 64 of them is repaired anyway — its stragglers
             // never store anything but final values)
             const uint64_t t0 = (uint64_t)wall_clock64();
-            while ((uint32_t)(__hip_atomic_load(ex.ctl + RS_EXIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ex.xbase) < ex.G - 1u &&
-                   (uint64_t)wall_clock64() - t0 < 64 * ex.spin)
+            for (;;) {
+                uint32_t out_n = 0;
+                for (int r = 0; r < RS_NG; ++r)
+                    out_n += __hip_atomic_load(ex.ctl + RS_XGRP + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (out_n - ex.xbase >= ex.G - 1u || (uint64_t)wall_clock64() - t0 >= 64 * ex.spin) break;
                 __builtin_amdgcn_s_sleep(8);
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         __syncthreads();
         rs_repair(ex.x, ex.d, ex.K, ex.tie_hi, ex.thr, ex.krem, ex.tiecut, ex.flags, ex.out, ex.ctl, h, scratch, wsum);
         __syncthreads();
-        if (t == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_fetch_add(ex.ctl + RS_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        count_out();
     }
 done:
 #ifdef FLC_RS_PRINT
@@ -3242,7 +3251,7 @@ static bool cs_single() {            // tuning runs: FLC_CS_SINGLE=1 keeps the o
 struct RsCtx {
     uint32_t* ctl = nullptr;
     uint32_t seq = 0;                   // launches so far (tags the tie counts of each call)
-    uint32_t xcum = 0;                  // workgroups launched so far (RS_EXIT's count before a launch)
+    uint32_t xcum = 0;                  // workgroups launched so far (the RS_XGRP counters' sum before a launch)
     hipStream_t last = nullptr;
     hipEvent_t done = nullptr;
 };
