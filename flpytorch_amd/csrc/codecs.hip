@@ -847,30 +847,51 @@ int selftest_division(const float* d_b, int nb, unsigned long long* d_bad, hipSt
 // 8 lane accumulators, lane l taking x[8k + l]^2 in order as fused multiply-adds, the 8 lanes
 // summed left to right, the D % 8 tail elements' squares added in order (fused), then the
 // correctly rounded square root.  Each lane's sum is one chain of D / 8 dependent fmas, which
-// no reassociation may shorten: one workgroup per row, wave 0's lanes 0..7 run the chains out
-// of LDS while waves 1..3 stream the row into a double buffer (transposed so that a chain reads
-// 4 consecutive steps per ds_read_b128).  Latency-bound by design (~3 M dependent fmas per
-// chain at D = 25 M): the parity mode of the drop-in, not a fast path.
+// no reassociation may shorten, so the kernel is built around that chain: one workgroup per row,
+// wave 0's lanes 0..7 run the 8 chains out of LDS (transposed: a chain's 4 next steps are one
+// ds_read_b128, 8 of them in flight) while waves 1..3 stream the next TN_CH elements into the
+// other half of a double buffer with every float4 load of the chunk in flight at once (the
+// previous form issued them a few at a time: 52.4 ms per call at D = 25 M, the chain waiting on
+// the staging; a single-wave register ring, every step's 4-byte load issued 64 steps ahead, 33.4
+// ms — a block of 64 steps does not cover one HBM latency).  Latency-bound by design: the parity
+// mode of the drop-in, not a fast path.
 // ------------------------------------------------------------------------------------------
-constexpr int TN_CH = 8192;                 // elements per staged chunk
+constexpr int TN_CH = 16384;                // elements per staged chunk (2048 steps of each chain)
 constexpr int TN_ST = TN_CH / 8 + 4;        // LDS stride of a lane's steps (+4: conflict-free staging)
+constexpr int TN_LD = (TN_CH / 4 + 191) / 192;   // float4 loads per staging thread and chunk
 
 __global__ __launch_bounds__(256) void k_norm_torch(const float* __restrict__ base, int64_t ld, int64_t d,
                                                     float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float buf[2][8 * TN_ST];
+    extern __shared__ __attribute__((aligned(16))) float tn_buf[];      // [2][8 * TN_ST]
     const int t = threadIdx.x;
     const int64_t row = blockIdx.x;
     const float* r = base + row * ld;
     const int64_t m = d - d % 8;                              // the lane accumulators' elements
     const int64_t nc = (m + TN_CH - 1) / TN_CH;
-    // waves 1..3 stage chunk c (zeros past m: fmaf(0, 0, a) == a for every a, so the padding
-    // leaves the chains' bits unchanged)
+    // waves 1..3 stage chunk c: every float4 load first (range-checked: zeros past m, and
+    // fmaf(0, 0, a) == a for the non-negative accumulators), then the transposed LDS writes
     auto stage = [&](int64_t c) {
-        float* b = buf[c & 1];
+        float* b = tn_buf + (c & 1) * 8 * TN_ST;
         const int64_t j0 = c * TN_CH;
-        for (int i = t - 64; i < TN_CH; i += 192) {
-            const int64_t j = j0 + i;
-            b[(i & 7) * TN_ST + (i >> 3)] = j < m ? __builtin_nontemporal_load(r + j) : 0.f;
+        const int64_t left = m - j0;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r + j0), (short)0,
+                                                          (int)(left >= TN_CH ? TN_CH * 4 : left * 4), 0x00020000);
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        u4v q[TN_LD];
+        const int p = t - 64;                                  // 0..191
+#pragma unroll
+        for (int u = 0; u < TN_LD; ++u) {
+            const int f = p + u * 192;                         // float4 index in the chunk
+            q[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(f < TN_CH / 4 ? f : 0) * 16u, 0, 2);
+        }
+#pragma unroll
+        for (int u = 0; u < TN_LD; ++u) {
+            const int f = p + u * 192;
+            if (f < TN_CH / 4) {
+                const int k = f >> 1, l0 = (f & 1) * 4;        // elements 4f .. 4f+3 = steps k of lanes l0 ..
+#pragma unroll
+                for (int e = 0; e < 4; ++e) b[(l0 + e) * TN_ST + k] = __uint_as_float(q[u][e]);
+            }
         }
     };
     float acc = 0.f;
@@ -880,14 +901,24 @@ __global__ __launch_bounds__(256) void k_norm_torch(const float* __restrict__ ba
         if (t >= 64) {
             if (c + 1 < nc) stage(c + 1);
         } else if (t < 8) {
-            const float4* b4 = reinterpret_cast<const float4*>(buf[c & 1] + t * TN_ST);
-#pragma unroll 8
-            for (int s = 0; s < TN_CH / 32; ++s) {
-                const float4 v = b4[s];
-                acc = fmaf(v.x, v.x, acc);
-                acc = fmaf(v.y, v.y, acc);
-                acc = fmaf(v.z, v.z, acc);
-                acc = fmaf(v.w, v.w, acc);
+            const float4* b4 = reinterpret_cast<const float4*>(tn_buf + (c & 1) * 8 * TN_ST + t * TN_ST);
+            constexpr int R = 8;                               // ds_read_b128 in flight
+            float4 cur[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) cur[u] = b4[u];
+            for (int s = 0; s < TN_CH / 32; s += R) {
+                float4 nxt[R];
+#pragma unroll
+                for (int u = 0; u < R; ++u) nxt[u] = b4[(s + R + u) % (TN_CH / 32)];   // (the wrap re-reads: harmless)
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    acc = fmaf(cur[u].x, cur[u].x, acc);
+                    acc = fmaf(cur[u].y, cur[u].y, acc);
+                    acc = fmaf(cur[u].z, cur[u].z, acc);
+                    acc = fmaf(cur[u].w, cur[u].w, acc);
+                }
+#pragma unroll
+                for (int u = 0; u < R; ++u) cur[u] = nxt[u];
             }
         }
         __syncthreads();
@@ -905,7 +936,11 @@ __global__ __launch_bounds__(256) void k_norm_torch(const float* __restrict__ ba
 int norm_torch_run(const float* x, int64_t ld, int64_t n, int64_t d, float* out, hipStream_t st) {
     if (n <= 0) return FLC_OK;
     ProfScope _ps("k_norm_torch", st);
-    hipLaunchKernelGGL(k_norm_torch, dim3((unsigned)n), dim3(256), 0, st, x, ld, d, out);
+    const size_t lds = 2 * 8 * TN_ST * sizeof(float);          // 128 KB: the double buffer
+    static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_norm_torch),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+    if (!ok) { set_error("k_norm_torch: %zu bytes of dynamic LDS refused", lds); return FLC_ERR_HIP; }
+    hipLaunchKernelGGL(k_norm_torch, dim3((unsigned)n), dim3(256), lds, st, x, ld, d, out);
     FLC_CHECK_LAUNCH("k_norm_torch");
     return FLC_OK;
 }
