@@ -477,7 +477,7 @@ def dropin(args):
     # per-kernel device time of one compressVector, over every client's row (flc_profile scopes)
     kernels = ["k_topk_sample", "k_topk_filter", "k_cand_select", "k_topk_exact_rows", "k_chunk_accum",
                "k_norm_partials", "k_ew_accum_vec", "k_ew_encode", "k_randk_scatter_dev", "k_assign_scatter",
-               "k_assign_finish", "k_lone_dither", "k_lone_resident", "k_norm_torch"]
+               "k_assign_finish", "k_lone_dither", "k_lone_resident", "k_norm_torch", "k_tn_sums", "k_tn_maps", "k_tn_walk"]
     _lib.profile_enable(True)
     for k in kernels:
         _lib.profile_collect(k)

@@ -22,7 +22,7 @@ FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
 # execution hints (flc_codec_params.flags): how, never what — every choice gives the same bits
 FLC_PATH_AUTO, FLC_PATH_SPARSE, FLC_PATH_DENSE = 0, 1, 2
 FLC_TIE_LOWEST, FLC_TIE_HIGHEST = 0, 1
-ABI_VERSION = 102
+ABI_VERSION = 103
 
 
 def FLC_ROW_GROUPS(g):
@@ -44,6 +44,7 @@ EXPORTS = [
     "flc_device_randk_counts_workspace_size", "flc_device_randk_counts",
     "flc_profile_enable", "flc_profile_collect", "flc_select_row_flags",
     "flc_selftest_division", "flc_norm2_torch_cpu", "flc_debug_resident",
+    "flc_norm2_torch_cpu_workspace_size", "flc_norm2_torch_cpu_ws",
 ]
 
 
@@ -178,6 +179,10 @@ def _bind(lib):
     lib.flc_selftest_division.argtypes = [vp, i32, vp, vp]
     if hasattr(lib, "flc_norm2_torch_cpu"):         # (absent from A/B builds of older revisions)
         lib.flc_norm2_torch_cpu.argtypes = [vp, i64, i64, i64, vp, vp]
+    if hasattr(lib, "flc_norm2_torch_cpu_ws"):      # (absent from A/B builds of older revisions)
+        lib.flc_norm2_torch_cpu_workspace_size.argtypes = [i64, i64]
+        lib.flc_norm2_torch_cpu_workspace_size.restype = sz
+        lib.flc_norm2_torch_cpu_ws.argtypes = [vp, i64, i64, i64, vp, vp, sz, vp]
     if hasattr(lib, "flc_debug_resident"):          # (absent from A/B builds of older revisions)
         lib.flc_debug_resident.argtypes = [i32, i64]
     if hasattr(lib, "flc_select_row_flags"):        # (absent from A/B builds of older revisions)
@@ -189,7 +194,8 @@ def _bind(lib):
                         "flc_encode_workspace_size", "flc_encode_reduce_workspace_size",
                         "flc_encode_shift_workspace_size", "flc_payload_bytes", "flc_pack_workspace_size",
                         "flc_unpack_reduce_workspace_size", "flc_combine_workspace_size",
-                        "flc_combine_blocks_workspace_size", "flc_device_randk_counts_workspace_size"):
+                        "flc_combine_blocks_workspace_size", "flc_device_randk_counts_workspace_size",
+                        "flc_norm2_torch_cpu_workspace_size"):
             getattr(lib, name).restype = i32
     return lib
 

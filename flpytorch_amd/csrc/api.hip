@@ -72,7 +72,7 @@ static int bad_params(const flc_codec_params* prm, const char* what) {
 
 using namespace flc;
 
-extern "C" int flc_version(void) { return 102; }   // 1.02: flc_debug_resident (1.01: flc_codec_params.tie, flc_norm2_torch_cpu)
+extern "C" int flc_version(void) { return 103; }   // 1.03: flc_norm2_torch_cpu_ws (1.02: flc_debug_resident; 1.01: tie, flc_norm2_torch_cpu)
 
 #ifndef FLC_SRC_HASH
 #define FLC_SRC_HASH "unknown"
@@ -115,6 +115,20 @@ extern "C" int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int6
                                     size_t ws_bytes, uint32_t* d_flags, void* stream) {
     if (!prm || (n > 0 && (!d_workspace || !d_flags))) { set_error("flc_select_row_flags: null argument"); return FLC_ERR_ARG; }
     return sel_row_flags(prm, n, d, d_workspace, ws_bytes, d_flags, (hipStream_t)stream);
+}
+
+extern "C" size_t flc_norm2_torch_cpu_workspace_size(int64_t n, int64_t d) {
+    return (n <= 0 || d < 0) ? 0 : norm_torch_ws_bytes(n, d);
+}
+
+extern "C" int flc_norm2_torch_cpu_ws(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* d_ws,
+                                      size_t ws_bytes, void* stream) {
+    if (n < 0 || d < 0 || (n > 1 && ld < d) || (n > 0 && (!d_rows || !d_out || !d_ws))) {
+        set_error("flc_norm2_torch_cpu_ws: bad args (n=%lld d=%lld ld=%lld)", (long long)n, (long long)d, (long long)ld);
+        return FLC_ERR_ARG;
+    }
+    if (n == 0) return FLC_OK;
+    return norm_torch_ws_run(d_rows, ld, n, d, d_out, d_ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int flc_debug_resident(int grid_mult, int64_t spin_ticks) { return rs_debug(grid_mult, spin_ticks); }

@@ -178,6 +178,9 @@ inline int64_t group_row(int64_t n, int G, int g, int lastpct) {
     return n * cum / unit;
 }
 int norm_torch_run(const float* x, int64_t ld, int64_t n, int64_t d, float* out, hipStream_t st);
+size_t norm_torch_ws_bytes(int64_t n, int64_t d);
+int norm_torch_ws_run(const float* x, int64_t ld, int64_t n, int64_t d, float* out, void* wsp, size_t ws_bytes,
+                      hipStream_t st);
 size_t sel_workspace(const flc_codec_params* prm, int64_t n, int64_t d);
 int sel_run(const flc_codec_params* prm, const flc_pattern* pat, RowSrc rows, bool vec, int64_t n, int64_t d,
             bool assign, const float* w, float wt, float* out, void* wsp, size_t ws_bytes, hipStream_t st);

@@ -303,6 +303,15 @@ int flc_device_randk_counts(uint64_t seed, int64_t client0, int64_t n, int64_t d
  * fmas per lane: latency-bound (a parity mode; bench.py --dropin --norm-mode torch_cpu prices it). */
 int flc_norm2_torch_cpu(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* stream);
 
+/* The same norms, bit for bit, without the chain (ABI 1.03): while a lane's accumulator stays in
+ * one binade its rounding grid is fixed, so each step is A -> A + D(A mod 2) on that grid (two
+ * integers; the parity carries ties-to-even) and runs of steps compose associatively; the steps
+ * that cross a binade are taken as real fmas (torch_norm.hip).  Three launches, a workspace of
+ * flc_norm2_torch_cpu_workspace_size(n, d) bytes (per row ~24 bytes per 4096 elements); n <= 65535. */
+size_t flc_norm2_torch_cpu_workspace_size(int64_t n, int64_t d);
+int flc_norm2_torch_cpu_ws(const float* d_rows, int64_t ld, int64_t n, int64_t d, float* d_out, void* d_ws,
+                           size_t ws_bytes, void* stream);
+
 /* Self-test of the exact fast fp32 division the dithering kernels use: for each of the n
  * device divisors, every float numerator in [2^-80, 2^80] is divided both ways and the
  * mismatches are written to d_mismatches[n] (device).  Must be all zero. */
