@@ -44,7 +44,7 @@ constexpr int32_t TN_BIG = 1 << 30;          // saturated increment: "crosses, t
 constexpr int TN_XB = 1024;                  // steps per block: the walk's unit (a map each)
 constexpr int TN_BPP = TN_PS / TN_XB;        // blocks per part (one wave of k_tn_maps each)
 constexpr int TN_NOGRID = -1000;             // no predicted grid: the block has no map
-static_assert(TN_BPP == TN_T / 64, "k_tn_maps: one wave per block");
+constexpr double TN_MARGIN = 2e-4;           // a predicted range this close to a binade edge: no map
 
 struct TnMap {                               // A -> A + d[A & 1] on the grid 2^eu (valid != 0)
     int32_t d0, d1, eu, valid;
@@ -148,100 +148,108 @@ __device__ inline int tn_predict(double a, double b) {
     // the float64 sums (a misprediction is caught by k_tn_walk; the margin only makes it rare);
     // TN_NOGRID when the range may straddle a binade
     if (!(b == b && b < 0x1p127)) return TN_NOGRID;
-    if (b < 0x1p-125 * 0.999) return -149;
-    if (a < 0x1p-125 * 1.001) return TN_NOGRID;
+    if (b < 0x1p-125 * (1.0 - TN_MARGIN)) return -149;
+    if (a < 0x1p-125 * (1.0 + TN_MARGIN)) return TN_NOGRID;
     int e = 0;
     (void)frexp(a, &e);                                                // a = f 2^e, f in [0.5, 1): binade e - 1
     const double lo = ldexp(1.0, e - 1), hi = ldexp(1.0, e);
-    return (a >= lo * 1.001 && b < hi * 0.999) ? e - 1 - 23 : TN_NOGRID;
+    return (a >= lo * (1.0 + TN_MARGIN) && b < hi * (1.0 - TN_MARGIN)) ? e - 1 - 23 : TN_NOGRID;
 }
 
-// per (part, row): a map per BLOCK of TN_XB steps (wave w of the workgroup = block w of the part):
-// each thread sums then composes its TN_PS / TN_T consecutive steps of every lane, on the grid
-// predicted for its block from the float64 prefix of the parts before, the blocks before in this
-// part and its own block's sum; a wave's ordered shuffle tree gives the block's map
-__global__ __launch_bounds__(TN_T) void k_tn_maps(const float* __restrict__ base, int64_t ld, int64_t d, TnWs ws) {
-    __shared__ double pre[TN_T / 64][8], bsum[TN_T / 64][8];
+// per (part, row): a map per BLOCK of TN_XB steps.  1024 threads, each with 4 consecutive steps
+// of every lane in registers (8 loads in flight a thread, read once); block b = threads 256 b ..
+// 256 b + 255 (4 waves).  Each lane's grid predicted for the block from the float64 prefix of the
+// parts before, the blocks before in this part and the block's own sum; the steps composed on it,
+// then ordered: a wave's shuffle tree, then the block's 4 waves in order.
+constexpr int TN_MT = 1024;                  // threads of k_tn_maps
+constexpr int TN_MS = TN_PS / TN_MT;         // steps a thread (4)
+static_assert(TN_XB == (TN_MT / TN_BPP) * TN_MS, "k_tn_maps: a block is 256 threads' steps");
+
+__global__ __launch_bounds__(TN_MT) void k_tn_maps(const float* __restrict__ base, int64_t ld, int64_t d, TnWs ws) {
+    // per thread and lane: its steps' float64 sum, then (reused) its composite map — reduced in
+    // order by 32 threads (block b, lane l), one LDS column each: no shuffle chains
+    __shared__ double cell[TN_MT][8];
+    __shared__ double pre[8], bpre[TN_BPP][8], bsum[TN_BPP][8];
     const int64_t P = tn_parts(d), p = blockIdx.x, row = blockIdx.y;
-    const int t = threadIdx.x, wv = t >> 6, j = t & 63;
+    const int t = threadIdx.x, blk = t / (TN_MT / TN_BPP);
+    constexpr int TPB = TN_MT / TN_BPP;                                // threads per block (256)
     const float* r = base + row * ld;
     const int64_t steps = (d - d % 8) / 8;
-    // the prefix of the parts before (order irrelevant: a prediction)
-    {
-        double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int64_t q = t; q < p; q += TN_T)
-#pragma unroll
-            for (int l = 0; l < 8; ++l) s[l] += ws.sums[(row * P + q) * 8 + l];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            double v = s[l];
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-            if (j == 0) pre[wv][l] = v;
-        }
-    }
     const int64_t k0 = p * TN_PS, k1 = min(k0 + (int64_t)TN_PS, steps);
-    constexpr int PER = TN_PS / TN_T;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(r + 8 * k0), (short)0,
                                                       (int)((k1 - k0) * 32), 0x00020000);
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    // this block's sums (one wave per block)
-    {
-        double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = 0; i < PER; ++i) {
-            const uint32_t k = (uint32_t)(t * PER + i);
-            const u4v a = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 32u, 0, 2);
-            const u4v b = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 32u + 16u, 0, 2);
+    u4v va[TN_MS], vb[TN_MS];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const double va = (double)__uint_as_float(a[e]), vb = (double)__uint_as_float(b[e]);
-                s[e] += va * va;
-                s[4 + e] += vb * vb;
-            }
-        }
+    for (int i = 0; i < TN_MS; ++i) {                                  // past k1: zeros (identity steps)
+        const uint32_t k = (uint32_t)(t * TN_MS + i);
+        va[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 32u, 0, 2);
+        vb[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 32u + 16u, 0, 2);
+    }
+    {                                                                  // the parts before (a prediction):
+        double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};                       // one column of LDS per lane
+        for (int64_t q = t; q < p; q += TN_MT)
 #pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            double v = s[l];
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-            if (j == 0) bsum[wv][l] = v;
+            for (int l = 0; l < 8; ++l) s8[l] += ws.sums[(row * P + q) * 8 + l];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) cell[t][l] = s8[l];
+    }
+    __syncthreads();
+    if (t < 8) {
+        double a = 0;
+        for (int i = 0; i < TN_MT; ++i) a += cell[i][t];
+        pre[t] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        double v = 0;
+#pragma unroll
+        for (int i = 0; i < TN_MS; ++i) {
+            const double x = (double)__uint_as_float(l < 4 ? va[i][l & 3] : vb[i][l & 3]);
+            v += x * x;
         }
+        cell[t][l] = v;
+    }
+    __syncthreads();
+    if (t < 8 * TN_BPP) {                                              // block b's sum of lane l
+        const int b = t >> 3, l = t & 7;
+        double v = 0;
+        for (int i = b * TPB; i < (b + 1) * TPB; ++i) v += cell[i][l];
+        bsum[b][l] = v;
+    }
+    __syncthreads();
+    if (t < 8) {
+        double a = pre[t];
+        for (int b = 0; b < TN_BPP; ++b) { bpre[b][t] = a; a += bsum[b][t]; }
     }
     __syncthreads();
     int eu[8];
 #pragma unroll
+    for (int l = 0; l < 8; ++l) eu[l] = tn_predict(bpre[blk][l], bpre[blk][l] + bsum[blk][l]);
+    __syncthreads();                                                   // (cell reused for the maps)
+    int2* mc = reinterpret_cast<int2*>(&cell[0][0]);                   // [TN_MT][8]
+#pragma unroll
     for (int l = 0; l < 8; ++l) {
-        double a = 0;
-        for (int w = 0; w < TN_T / 64; ++w) a += pre[w][l];
-        for (int w = 0; w < wv; ++w) a += bsum[w][l];
-        eu[l] = tn_predict(a, a + bsum[wv][l]);
-    }
-    // compose this thread's steps (again from L2) on each lane's predicted grid
-    int32_t a0[8], a1[8];
+        int32_t a0 = 0, a1 = 0;
 #pragma unroll
-    for (int l = 0; l < 8; ++l) { a0[l] = 0; a1[l] = 0; }
-    for (int i = 0; i < PER; ++i) {
-        const uint32_t k = (uint32_t)(t * PER + i);
-        const u4v a = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 32u, 0, 2);     // past k1: zeros (identity)
-        const u4v b = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 32u + 16u, 0, 2);
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
+        for (int i = 0; i < TN_MS; ++i) {
             int32_t s0, s1;
-            tn_step(__uint_as_float(l < 4 ? a[l & 3] : b[l & 3]), eu[l], s0, s1);
-            tn_compose(a0[l], a1[l], s0, s1, a0[l], a1[l]);
+            tn_step(__uint_as_float(l < 4 ? va[i][l & 3] : vb[i][l & 3]), eu[l], s0, s1);
+            tn_compose(a0, a1, s0, s1, a0, a1);
         }
+        mc[t * 8 + l] = make_int2(a0, a1);
     }
-    // the wave's ordered tree: lane j takes lane j + o (its successor run) for o = 1, 2, 4, ..
-#pragma unroll
-    for (int l = 0; l < 8; ++l) {
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t q0 = __shfl_down(a0[l], o, 64), q1 = __shfl_down(a1[l], o, 64);
-            if ((j & (2 * o - 1)) == 0) tn_compose(a0[l], a1[l], q0, q1, a0[l], a1[l]);
+    __syncthreads();
+    if (t < 8 * TN_BPP) {                                              // block b's map of lane l, in order
+        const int b = t >> 3, l = t & 7;
+        int32_t a0 = 0, a1 = 0;
+        for (int i = b * TPB; i < (b + 1) * TPB; ++i) {
+            const int2 m = mc[i * 8 + l];
+            tn_compose(a0, a1, m.x, m.y, a0, a1);
         }
-    }
-    if (j == 0) {
-        const int64_t B = P * TN_BPP, blk = p * TN_BPP + wv;
-#pragma unroll
-        for (int l = 0; l < 8; ++l)
-            ws.maps[(row * 8 + l) * B + blk] = TnMap{a0[l], a1[l], eu[l], eu[l] != TN_NOGRID ? 1 : 0};
+        const int e = tn_predict(bpre[b][l], bpre[b][l] + bsum[b][l]);
+        ws.maps[(row * 8 + l) * (P * TN_BPP) + p * TN_BPP + b] = TnMap{a0, a1, e, e != TN_NOGRID ? 1 : 0};
     }
 }
 
@@ -250,71 +258,46 @@ __global__ __launch_bounds__(TN_T) void k_tn_maps(const float* __restrict__ base
 // ------------------------------------------------------------------------------------------
 constexpr int TN_WPL = TN_XB / 64;          // steps per wave lane in the exact pass over one block
 
-// the exact pass over steps [k0, k1) of lane l (k1 - k0 <= TN_XB), the accumulator uniform in the wave
-__device__ float tn_block_exact(const float* r, int l, int64_t k0, int64_t k1, float acc) {
+// the exact pass over steps [k0, k1) of lane l (k1 - k0 <= TN_XB), the accumulator uniform in the
+// wave: the block's values staged in LDS by the wave (16 loads a lane in flight), then the chain
+// itself, fmaf by fmaf, in one lane (4 values a ds_read_b128, 8 reads ahead): ~8 cycles a step
+// whatever the crossings (a map scan per crossing cost more: profiles/r06/norm/walk_probe.txt)
+__device__ float tn_block_exact(const float* r, int l, int64_t k0, int64_t k1, float acc, float* stage) {
     const int j = threadIdx.x & 63;
-    const int64_t js = k0 + (int64_t)j * TN_WPL;                     // this wave lane's first step
     float xv[TN_WPL];
 #pragma unroll
     for (int i = 0; i < TN_WPL; ++i) {
-        const int64_t k = js + i;
-        xv[i] = k < k1 ? r[8 * k + l] : 0.f;                           // (0: the identity step)
+        const int64_t k = k0 + (int64_t)i * 64 + j;                   // coalesced over the lanes
+        xv[i] = k < k1 ? r[8 * k + l] : 0.f;                           // (0: fmaf(0, 0, a) == a, a >= 0)
     }
-    int64_t cur = k0;
-    while (cur < k1) {
-        const uint32_t ab = __float_as_uint(acc);
-        if ((ab & 0x7FFFFFFFu) >= 0x7F800000u) break;                  // inf / NaN: the caller finishes
-                                                                        // (later blocks return it at once)
-        int eu;
-        int32_t A;
-        tn_grid(acc, eu, A);
-        // this wave lane's composite over its steps at or after cur
-        int32_t c0 = 0, c1 = 0;
 #pragma unroll
-        for (int i = 0; i < TN_WPL; ++i) {
-            if (js + i >= cur) {
-                int32_t s0, s1;
-                tn_step(xv[i], eu, s0, s1);
-                tn_compose(c0, c1, s0, s1, c0, c1);
-            }
-        }
-        // inclusive ordered scan over the wave lanes (Hillis-Steele: prefix of lanes < j, then mine)
-        int32_t p0 = c0, p1 = c1;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t q0 = __shfl_up(p0, o, 64), q1 = __shfl_up(p1, o, 64);
-            if (j >= o) tn_compose(q0, q1, p0, p1, p0, p1);
-        }
-        const int32_t end = A + ((A & 1) ? p1 : p0);                   // A after this lane's steps
-        const uint64_t cross = __ballot(end >= TN_AMAX);
-        if (!cross) {
-            acc = tn_value(__shfl(end, 63, 64), eu);
-            break;
-        }
-        const int jc = __ffsll((long long)cross) - 1;                  // the first lane that crosses
-        // A at its first step: the exclusive prefix (lane jc - 1's inclusive), then its steps one by one
-        const int32_t e0 = __shfl(p0, jc > 0 ? jc - 1 : 0, 64), e1 = __shfl(p1, jc > 0 ? jc - 1 : 0, 64);
-        int32_t As = jc > 0 ? A + ((A & 1) ? e1 : e0) : A;
-        float nacc = 0.f;
-        int64_t ncur = k1;
-        if (j == jc) {
+    for (int i = 0; i < TN_WPL; ++i) stage[i * 64 + j] = xv[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (j == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(stage);
+        constexpr int R = 8;
+        float4 cur[R];
 #pragma unroll
-            for (int i = 0; i < TN_WPL; ++i) {
-                if (js + i >= cur && ncur == k1) {
-                    int32_t s0, s1;
-                    tn_step(xv[i], eu, s0, s1);
-                    const int32_t nx = As + ((As & 1) ? s1 : s0);
-                    if (nx >= TN_AMAX) {                               // the crossing step: the real fma
-                        nacc = fmaf(xv[i], xv[i], tn_value(As, eu));
-                        ncur = js + i + 1;
-                    } else {
-                        As = nx;
-                    }
-                }
+        for (int u = 0; u < R; ++u) cur[u] = s4[u];
+        for (int q = 0; q < TN_XB / 4; q += R) {
+            float4 nxt[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) nxt[u] = s4[(q + R + u) % (TN_XB / 4)];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                acc = fmaf(cur[u].x, cur[u].x, acc);
+                acc = fmaf(cur[u].y, cur[u].y, acc);
+                acc = fmaf(cur[u].z, cur[u].z, acc);
+                acc = fmaf(cur[u].w, cur[u].w, acc);
             }
+#pragma unroll
+            for (int u = 0; u < R; ++u) cur[u] = nxt[u];
         }
-        acc = __shfl(nacc, jc, 64);
-        cur = (int64_t)__shfl((long long)ncur, jc, 64);
     }
+    acc = __shfl(acc, 0, 64);
+    __builtin_amdgcn_wave_barrier();                                   // (stage reused by the next block)
     return acc;
 }
 
@@ -329,6 +312,7 @@ constexpr int TN_G = 4;                      // blocks per wave lane in a window
 __global__ __launch_bounds__(64) void k_tn_walk(const float* __restrict__ base, int64_t ld, int64_t d, TnWs ws,
                                                 float* __restrict__ out) {
     __shared__ uint32_t last_s;
+    __shared__ __attribute__((aligned(16))) float stage[TN_XB];
     const int l = blockIdx.x;
     const int64_t row = blockIdx.y;
     const int j = threadIdx.x;
@@ -391,7 +375,7 @@ __global__ __launch_bounds__(64) void k_tn_walk(const float* __restrict__ base, 
         const uint64_t tx = (uint64_t)wall_clock64();
         ++n_ex;
 #endif
-        acc = tn_block_exact(r, l, q * TN_XB, min((q + 1) * TN_XB, steps), acc);   // block q exactly
+        acc = tn_block_exact(r, l, q * TN_XB, min((q + 1) * TN_XB, steps), acc, stage);   // block q exactly
 #ifdef FLC_TN_PRINT
         t_ex += (uint64_t)wall_clock64() - tx;
 #endif
@@ -457,7 +441,7 @@ int norm_torch_ws_run(const float* x, int64_t ld, int64_t n, int64_t d, float* o
         hipLaunchKernelGGL(k_tn_sums, dim3((unsigned)P, (unsigned)n), dim3(TN_T), 0, st, x, ld, d, ws); }
         FLC_CHECK_LAUNCH("k_tn_sums");
         { ProfScope _ps("k_tn_maps", st);
-        hipLaunchKernelGGL(k_tn_maps, dim3((unsigned)P, (unsigned)n), dim3(TN_T), 0, st, x, ld, d, ws); }
+        hipLaunchKernelGGL(k_tn_maps, dim3((unsigned)P, (unsigned)n), dim3(TN_MT), 0, st, x, ld, d, ws); }
         FLC_CHECK_LAUNCH("k_tn_maps");
     }
     if (P == 0) FLC_CHECK_HIP(hipMemsetAsync(ws.done, 0, (size_t)n * sizeof(uint32_t), st));   // (no k_tn_sums)
