@@ -695,6 +695,8 @@ def main():
                     help="server side from the wire format: decode+reduce of N resident payloads (own line, not value)")
     ap.add_argument("--norm-mode", default="exact", choices=["exact", "torch_cpu"],
                     help="--dropin: Compressor.norm_mode of the dithering codecs (torch_cpu: the reference's norm bits)")
+    ap.add_argument("--alloc", choices=["contiguous", "default"], default="contiguous",
+                    help="the resident rows' HBM: one physically contiguous range (flc_rows_alloc) or torch's allocator")
     ap.add_argument("--no-strong-c4", action="store_true",
                     help="skip the strong_c4 block (C4 at fixed N=4096, ordered combine) of the default line")
     ap.add_argument("--strong-steps", type=int, default=5, help="timed steps of the strong_c4 block")
@@ -772,7 +774,10 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     if not strong:
         n_dist = min(n, wl["pool"]) if mixed else n
-    rows = torch.empty((n_dist, d), dtype=torch.float32, device=dev)
+    # the resident client-update matrix in physically contiguous HBM (flpytorch_amd.resident: the
+    # default allocation's fragments read 6-10 % slower in places, more translation misses)
+    from flpytorch_amd.resident import resident_rows
+    rows, rows_alloc = resident_rows(n_dist, d, device=dev, contiguous=args.alloc == "contiguous")
     for i in range(0, n_dist, 64):
         rows[i:i + 64].normal_(generator=gen)
         if args.dist == "heavy":
@@ -920,12 +925,13 @@ def main():
         c4 = WORKLOADS["c4"]
         blk = c4["n_total"] // N_BLOCKS
         g4 = torch.Generator(device=dev).manual_seed(4096)          # the same rows on every rank
-        rows4 = torch.empty((blk, c4["d"]), dtype=torch.float32, device=dev)
+        rows4, alloc4 = resident_rows(blk, c4["d"], device=dev, contiguous=args.alloc == "contiguous")
         for i in range(0, blk, 64):
             rows4[i:i + 64].normal_(generator=g4)
         red4 = ag.UplinkReducer(ag.initCompressor(c4["spec"], c4["d"]), device=dev, seed=20241015)
         strong_c4 = strong_block(product_partial(red4), product_fold(), rows4, c4["n_total"], c4["d"], dev,
                                  steps=args.strong_steps, warmup=1, group=dist.group.WORLD if world > 1 else None)
+        strong_c4["rows_alloc"] = alloc4
         del rows4
 
     step_ms = elapsed / args.steps * 1e3
@@ -999,7 +1005,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic N(0,1) * 10^U(-3,3)" if args.dist == "heavy" else "synthetic N(0,1)")
-                    + " fp32 rows generated on device (seeded per rank); "
+                    + f" fp32 rows generated on device (seeded per rank) in {rows_alloc} HBM; "
                     + (f"compat patterns (the reference's numpy stream, resident in HBM; {compat_note})"
                        if args.compat else "device-RNG patterns")
                     + (f"; {n_dist} resident distinct rows replayed through the {n} clients' row pointers, "
@@ -1011,6 +1017,7 @@ def main():
                                     f"C{wl['config'] + 1} {'/'.join(specs) if mixed else spec} N={n}/GPU D={d}"),
                        "codec": "/".join(specs) if mixed else spec,
                        "clients_per_gpu": n, "clients_total": n_total if strong else n * world, "D": d, "K": k,
+                       "rows_alloc": rows_alloc,
                        "parallelism": f"client-shard dp{world}" + (
                            f" + {N_BLOCKS} block partials, all-to-all + block-order fold + all-gather (G-invariant)"
                            if strong else (" + RCCL all-reduce" if world > 1 else ""))},

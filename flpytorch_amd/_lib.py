@@ -22,7 +22,7 @@ FLC_REDUCE_PLAIN, FLC_REDUCE_REL_X = 0, 1
 # execution hints (flc_codec_params.flags): how, never what — every choice gives the same bits
 FLC_PATH_AUTO, FLC_PATH_SPARSE, FLC_PATH_DENSE = 0, 1, 2
 FLC_TIE_LOWEST, FLC_TIE_HIGHEST = 0, 1
-ABI_VERSION = 103
+ABI_VERSION = 104
 
 
 def FLC_ROW_GROUPS(g):
@@ -44,7 +44,7 @@ EXPORTS = [
     "flc_device_randk_counts_workspace_size", "flc_device_randk_counts",
     "flc_profile_enable", "flc_profile_collect", "flc_select_row_flags",
     "flc_selftest_division", "flc_norm2_torch_cpu", "flc_debug_resident",
-    "flc_norm2_torch_cpu_workspace_size", "flc_norm2_torch_cpu_ws",
+    "flc_norm2_torch_cpu_workspace_size", "flc_norm2_torch_cpu_ws", "flc_rows_alloc", "flc_rows_free",
 ]
 
 
@@ -183,6 +183,9 @@ def _bind(lib):
         lib.flc_norm2_torch_cpu_workspace_size.argtypes = [i64, i64]
         lib.flc_norm2_torch_cpu_workspace_size.restype = sz
         lib.flc_norm2_torch_cpu_ws.argtypes = [vp, i64, i64, i64, vp, vp, sz, vp]
+    if hasattr(lib, "flc_rows_alloc"):              # (absent from A/B builds of older revisions)
+        lib.flc_rows_alloc.argtypes = [sz, i32, vp]
+        lib.flc_rows_free.argtypes = [vp]
     if hasattr(lib, "flc_debug_resident"):          # (absent from A/B builds of older revisions)
         lib.flc_debug_resident.argtypes = [i32, i64]
     if hasattr(lib, "flc_select_row_flags"):        # (absent from A/B builds of older revisions)

@@ -72,7 +72,7 @@ static int bad_params(const flc_codec_params* prm, const char* what) {
 
 using namespace flc;
 
-extern "C" int flc_version(void) { return 103; }   // 1.03: flc_norm2_torch_cpu_ws (1.02: flc_debug_resident; 1.01: tie, flc_norm2_torch_cpu)
+extern "C" int flc_version(void) { return 104; }   // 1.04: flc_rows_alloc / free (1.03: flc_norm2_torch_cpu_ws; 1.02: flc_debug_resident; 1.01: tie, flc_norm2_torch_cpu)
 
 #ifndef FLC_SRC_HASH
 #define FLC_SRC_HASH "unknown"
@@ -115,6 +115,30 @@ extern "C" int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int6
                                     size_t ws_bytes, uint32_t* d_flags, void* stream) {
     if (!prm || (n > 0 && (!d_workspace || !d_flags))) { set_error("flc_select_row_flags: null argument"); return FLC_ERR_ARG; }
     return sel_row_flags(prm, n, d, d_workspace, ws_bytes, d_flags, (hipStream_t)stream);
+}
+
+// Host helper (no compute): the resident client-update matrix in PHYSICALLY CONTIGUOUS HBM
+// (hipDeviceMallocContiguous).  A default allocation of tens of GB is stitched from fragments and
+// some of its rows read 6-10 % slower, with more address-translation misses (profiles/r06/
+// regions_pmc.jsonl); contiguous memory maps with the largest page fragments: C4's 51.2 GB shard
+// read 8.04 vs 8.48 ms, its step 9.09 vs 9.57 ms, same process (profiles/r06/contig.jsonl).
+extern "C" int flc_rows_alloc(size_t bytes, int contiguous, void** d_ptr) {
+    if (!d_ptr || bytes == 0) { set_error("flc_rows_alloc: bad args"); return FLC_ERR_ARG; }
+    *d_ptr = nullptr;
+    const hipError_t e = contiguous ? hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous) : hipMalloc(d_ptr, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *d_ptr = nullptr;
+        set_error("flc_rows_alloc: %s of %zu bytes failed: %s", contiguous ? "contiguous allocation" : "hipMalloc", bytes,
+                  hipGetErrorString(e));
+        return FLC_ERR_HIP;
+    }
+    return FLC_OK;
+}
+
+extern "C" int flc_rows_free(void* d_ptr) {
+    if (d_ptr && hipFree(d_ptr) != hipSuccess) { set_error("flc_rows_free: hipFree failed"); return FLC_ERR_HIP; }
+    return FLC_OK;
 }
 
 extern "C" size_t flc_norm2_torch_cpu_workspace_size(int64_t n, int64_t d) {

@@ -342,6 +342,17 @@ int flc_profile_collect(const char* kernel, double* h_total_ms, int64_t* h_launc
 int flc_select_row_flags(const flc_codec_params* prm, int64_t n, int64_t d, const void* d_workspace,
                          size_t ws_bytes, uint32_t* d_flags, void* stream);
 
+/* Host helper (no compute; the compute entries still never allocate): storage for the resident
+ * client-update matrix.  contiguous != 0: physically contiguous HBM (hipDeviceMallocContiguous) —
+ * a default allocation of tens of GB is stitched from fragments and some of its rows read 6-10 %
+ * slower with more address-translation misses; contiguous memory maps with the largest fragments
+ * (C4's shard: plain read 8.04 vs 8.48 ms, encode+reduce step 9.09 vs 9.57 ms, one process).
+ * FLC_ERR_HIP when the allocation fails (e.g. no contiguous range that large is free): the caller
+ * may fall back to contiguous = 0.  Free with flc_rows_free.  (The reference keeps its N client
+ * tensors wherever torch puts them, model_funcs.py:367-386.) */
+int flc_rows_alloc(size_t bytes, int contiguous, void** d_ptr);
+int flc_rows_free(void* d_ptr);
+
 /* Test hook of the lone-TopK resident selection (no compute): the next resident launches of this
  * process use grid_mult x their grid (grid_mult > 1: more 1024-thread workgroups than can be
  * resident at once, so the call's grid waits give up and its abort + exact repair path runs) and

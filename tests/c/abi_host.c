@@ -7,7 +7,7 @@
 #include "flcodec.h"
 
 int main(void) {
-    if (flc_version() != 103) { printf("bad version\n"); return 1; }
+    if (flc_version() != 104) { printf("bad version\n"); return 1; }
     flc_codec_params prm;
     memset(&prm, 0, sizeof(prm));
     prm.codec = FLC_TOPK;

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.flc_version() == _lib.ABI_VERSION == 103
+    assert lib.flc_version() == _lib.ABI_VERSION == 104
 
 
 def test_library_build_id_matches_tree():
