@@ -148,3 +148,23 @@ def test_resident_compressvector_threads_distinct_streams():
         assert f & 16 and not f & 1, f"thread {i}: flags {f}"
         for o in outs:
             assert np.array_equal(o.cpu().numpy().view(np.uint32), want[i].cpu().numpy().view(np.uint32))
+
+
+def test_workspace_keeps_a_bounded_number_of_streams():
+    """the per-stream scratch is an LRU of _lib.Workspace.MAX_STREAMS streams —
+    a pool that makes a stream per worker call does not keep one buffer per stream ever seen; the
+    calls on every stream stay exact."""
+    from flpytorch_amd import _lib
+    from flpytorch_amd import aggregation as ag
+    from oracle import codecs as oc
+    d = 100_003
+    x = torch.randn(d, generator=torch.Generator(device="cuda").manual_seed(2), device="cuda")
+    want = oc.OracleCompressor("topk:1%", d).compress(x.cpu().numpy())
+    _lib.WORKSPACE.release()
+    streams = [torch.cuda.Stream() for _ in range(_lib.Workspace.MAX_STREAMS + 8)]
+    for s in streams:
+        with torch.cuda.stream(s):
+            got = ag.initCompressor("topk:1%", d).compressVector(x)
+        s.synchronize()
+        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    assert len(_lib.WORKSPACE._bufs) <= _lib.Workspace.MAX_STREAMS
