@@ -64,6 +64,7 @@ constexpr int RS_XGRP = RS_GRP + 32 * RS_NG_MAX;  // per group: workgroups count
 constexpr int RS_ABV = RS_XGRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
 constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
+constexpr int RS_SR = 8;              // replicas of the sample's histogram (LDS)
 #ifndef FLC_RS_STPOL
 #define FLC_RS_STPOL 2                // the dense output's stores: nontemporal (2) or default (0)
 #endif
@@ -79,18 +80,34 @@ constexpr int RS_SS = 8192;           // the speculative first digit's sample (3
 #ifndef FLC_RS_G0REL
 #define FLC_RS_G0REL 1                // workgroup 0 releases the row state before it counts out
 #endif
+#ifndef FLC_RS_FENCE
+// k_lone_resident's grid rounds: 1 = agent-scope release / acquire fences around the counters (an
+// L2 write-back or L1 invalidate each, ~1.7 us; five on the last arriver's path); 0 = no fences —
+// every byte handed over inside the launch is written by an agent-scope atomic (histogram adds,
+// list entries, counters, the release word) and read by agent-scope (sc1) loads, every writing
+// wave drains (vmcnt(0)) before its workgroup's one counter add, and the counters never need a
+// reset store (see rs_arrive)
+#define FLC_RS_FENCE 0
+#endif
 #ifndef FLC_RS_SPEC
 #define FLC_RS_SPEC 1                 // k_lone_resident: speculative first digit (two digits in one round)
 #endif
 constexpr int RS_HREP = RS_ABV + 32 * RS_NG_MAX;
 constexpr int RS_HSPEC = RS_HREP + 3 * RS_NG * HBINS;    // [RS_NG][3][HBINS] speculative second digit
 constexpr int RS_CLIST = RS_HSPEC + 3 * RS_NG * HBINS;   // [RS_CAP] (value bits, index)
-constexpr int RS_TCNT = RS_CLIST + 2 * RS_CAP;
+constexpr int RS_TCNT = RS_CLIST + 2 * RS_CAP;               // (tie counts: 64-bit (call << 32 | count) per workgroup)
+constexpr int RS_GMAX = 1024;                                  // workgroups a launch may have (tie counts, list slots)
+constexpr int RS_CS = 4;                                       // listed elements a workgroup keeps in slots of its own
+constexpr int RS_CNUM = RS_TCNT + 2 * RS_GMAX;                 // [RS_GMAX] elements a workgroup listed (this call)
+constexpr int RS_CREG = RS_CNUM + RS_GMAX;                     // [RS_GMAX][RS_CS] 64-bit (value bits, index)
 #ifdef FLC_RS_PRINT
-constexpr int RS_PROBE = RS_TCNT + 2048;   // probe builds: per-workgroup start / arrival stamps
+constexpr int RS_PROBE = RS_CREG + 2 * RS_CS * RS_GMAX;        // probe builds: per-workgroup phase stamps
 constexpr int RS_CTL = RS_PROBE + 4096;
 #else
-constexpr int RS_CTL = RS_TCNT + 2048;     // (tie counts: 64-bit (call << 32 | count) per workgroup)
+constexpr int RS_CTL = RS_CREG + 2 * RS_CS * RS_GMAX;
+#endif
+#ifndef FLC_RS_SPECST
+#define FLC_RS_SPECST 0               // 1: the dense output outside the speculative window stored during the round (slower: 42.5 vs 36.7 us, the writes delay the merger)
 #endif
 #ifndef FLC_CS_LIST
 #define FLC_CS_LIST 1
@@ -2452,9 +2469,10 @@ __device__ inline bool rs_arrive(const RsTree& tr, uint32_t* flag_s, uint32_t* g
     __syncthreads();
     if (threadIdx.x == 0) {
         *gen_s = gen;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (FLC_RS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         uint32_t last = 0;
         uint32_t* gc = tr.ctl + RS_GRP + 32 * tr.grp;
+#if FLC_RS_FENCE
         if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tr.gsz - 1u) {
             // the group's members' writes (released before their arrivals) ordered before this
             // workgroup's release into the global counter: acquire, then release (transitivity)
@@ -2467,6 +2485,26 @@ __device__ inline bool rs_arrive(const RsTree& tr, uint32_t* flag_s, uint32_t* g
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
         }
+#else
+        // Write-through hand-off: every member drained its atomics before its add, so when an add
+        // RETURNS the members counted before it have their bytes at the coherence point, and a
+        // group's last add comes before that workgroup's global add (it waits for the value).
+        // The counters are never stored to: an arrival is the last of its round when it takes the
+        // count to a multiple of the group size, and that workgroup takes the group size back off
+        // with an add — adds commute, so whenever that add lands (before or among the next
+        // round's arrivals, which start only after this round's release) the next round's
+        // arrivals still return every residue mod the size once, the last one gsz - 1.
+        const uint32_t o = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((o + 1u) % tr.gsz == 0u) {
+            __hip_atomic_fetch_add(gc, 0u - tr.gsz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t og = __hip_atomic_fetch_add(tr.ctl + RS_GLOB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((og + 1u) % tr.ngr == 0u) {
+                __hip_atomic_fetch_add(tr.ctl + RS_GLOB, 0u - tr.ngr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");              // (compiler order only)
+#endif
         *flag_s = last;
     }
     __syncthreads();
@@ -2477,7 +2515,8 @@ __device__ inline void rs_release(const RsTree& tr, const uint32_t* gen_s, uint6
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // (the waiters read nothing but this word: its payload is the round's result)
+        if (FLC_RS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_store(reinterpret_cast<uint64_t*>(tr.ctl + RS_GEN), (uint64_t)((*gen_s + 1u) & 7u) | (payload << 3),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2487,7 +2526,7 @@ __device__ inline void rs_release(const RsTree& tr, const uint32_t* gen_s, uint6
 // workgroup to abort, *rep_s = 1, repairs it) or another workgroup's did (RS_GAVE holds the
 // call's sequence number): the caller leaves at once.
 __device__ inline bool rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t* res_s, uint32_t* ok_s,
-                               uint32_t* rep_s, uint64_t spin, uint32_t seq) {
+                               uint32_t* rep_s, uint64_t spin, uint32_t seq, bool raw_bar = false) {
     if (threadIdx.x == 0) {
         const uint64_t* rw = reinterpret_cast<const uint64_t*>(tr.ctl + RS_GEN);
         uint32_t* ab = tr.ctl + RS_GAVE;
@@ -2508,12 +2547,19 @@ __device__ inline bool rs_wait(const RsTree& tr, const uint32_t* gen_s, uint32_t
                 break;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (FLC_RS_FENCE || !ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");      // (compiler order only)
         res_s[0] = (uint32_t)(w >> 3);
         res_s[1] = (uint32_t)(w >> 35);
         *ok_s = ok;
     }
-    __syncthreads();
+    if (raw_bar) {                     // (the other waves' stores in flight stay in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    } else {
+        __syncthreads();
+    }
     return *ok_s != 0u;
 }
 
@@ -2593,6 +2639,9 @@ __device__ inline void rs_repair(const float* x, uint32_t d, uint32_t K, uint32_
 }
 
 #ifdef FLC_RS_PRINT                       // probe builds: phase stamps of workgroup 0 (printf)
+#ifndef FLC_RS_TLK
+#define FLC_RS_TLK 0, 4, 1, 2, 3, 10, 12   // the 7 stamps the timeline reports (13: the merger flag)
+#endif
 #define RS_STAMP(i) do { if (threadIdx.x == 0) stamp[i] = (uint64_t)wall_clock64(); } while (0)
 #else
 #define RS_STAMP(i) do { } while (0)
@@ -2608,6 +2657,26 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     const uint32_t G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
 #ifdef FLC_RS_PRINT
     uint64_t stamp[16] = {0};
+    // every 16th call, workgroup 0 summarises the PREVIOUS call's per-workgroup timeline (complete:
+    // that launch has ended), so that the stamps are of back-to-back calls, not of a cold launch
+    if (g == 0 && t == 0 && (seq & 15u) == 0u && G <= 256u) {
+        const uint64_t* pr = reinterpret_cast<const uint64_t*>(ctl + RS_PROBE);
+        const int ks[7] = {FLC_RS_TLK};
+        uint64_t s0 = ~0ull;
+        for (uint32_t i = 0; i < G; ++i) { const uint64_t v = pr[i]; s0 = v < s0 ? v : s0; }
+        uint32_t mg = 0;
+        for (uint32_t i = 0; i < G; ++i) if (pr[7 * 256 + i]) mg = i;
+        printf("rs_tl G=%u merger %u (x10ns from the first start): ", G, mg);
+        for (int k = 0; k < 7; ++k) {
+            uint64_t mn = ~0ull, mx = 0, sum = 0;
+            for (uint32_t i = 0; i < G; ++i) {
+                const uint64_t v = pr[k * 256 + i] - s0;
+                mn = v < mn ? v : mn; mx = v > mx ? v : mx; sum += v;
+            }
+            printf("s%d %llu/%llu/%llu ", ks[k], mn, sum / G, mx);
+        }
+        printf("\n");
+    }
 #endif
     RS_STAMP(0);
     RsTree tr;
@@ -2622,6 +2691,8 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     // repairer knows when this call's others are out (sum - xbase == G - 1) and a clean call needs
     // to know nothing.
     auto count_out = [&]() {
+        // (after this lane's counter adds have landed: a repair zeroes the counters once all are out)
+        if (t == 0 && !FLC_RS_FENCE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (t == 0 && !FLC_RS_PROBE_NOCOUNT)
             __hip_atomic_fetch_add(ctl + RS_XGRP + 32 * tr.grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
@@ -2643,8 +2714,14 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                       G, xbase, spin};
     }
     const uint32_t nb = (uint32_t)(d * 4);                               // d <= RS_U * 4096 * CUs
-    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows.row_s(0)), (short)0, (int)nb, 0x00020000);
-    const auto ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)nb, 0x00020000);
+    // the output's descriptor, rebuilt where the stores are from the LDS copy of the arguments (one
+    // kept from here to the end of the kernel was spilled and shuffled around every store)
+    auto out_rsrc = [&]() {
+        const uint64_t op = reinterpret_cast<uint64_t>(ex_s.out);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)op), hi = __builtin_amdgcn_readfirstlane((uint32_t)(op >> 32));
+        const uint32_t nbx = __builtin_amdgcn_readfirstlane(ex_s.d * 4u);
+        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), (short)0, (int)nbx, 0x00020000);
+    };
     // float4 u of this thread: elements 4 (g e4 RS_NT + u RS_NT + t) + q, coalesced over the threads;
     // index order inside the workgroup is (u, t, q), workgroups in order (G = ceil(d / (4 e4 RS_NT))).
     // A thread's float4 u < uv lie (at least partly) inside the row; the rest are skipped.  The one
@@ -2685,29 +2762,78 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         const auto q = __builtin_amdgcn_raw_buffer_load_b128(rxg, t * 16u, u * RS_NT * 16, FLC_LOADPOL);
         v[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
     }
+#ifdef FLC_RS_PRINT
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                    // (probe: when the row has landed)
+    RS_STAMP(4);
+#endif
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 3                             // (cost probe: the loads, then the row stored)
+    {
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        const uint64_t op = reinterpret_cast<uint64_t>(out);
+        const auto rq = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(op), (short)0, (int)nb, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < RU; ++u)
+            if (u < uv) {
+                const u4v ov = {__float_as_uint(v[u].x), __float_as_uint(v[u].y), __float_as_uint(v[u].z), __float_as_uint(v[u].w)};
+                __builtin_amdgcn_raw_buffer_store_b128(ov, rq, voff, u * RS_NT * 16, FLC_RS_STPOL);
+            }
+        return;
+    }
+#endif
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 1                             // (cost probe: the loads only)
+    {
+        uint32_t a = 0;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) a |= __float_as_uint(v[u].x);
+        if (a == 0x7FFFFFFFu) out[0] = 1.f;
+        return;
+    }
+#endif
     uint32_t prefix = 0, krem = (uint32_t)K, last = 0, bar = 0;
     bool cand = false;
     uint32_t bs = 0;
     int p0 = 0;
+    // bit u: float4 u holds an element whose first digit is in the speculative window (bs +- 1);
+    // the others were stored before the round's release when the guess hits (FLC_RS_SPECST)
+    uint32_t winm = 0;
+    bool sst = false;                                                    // (uniform) those stores made and final
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     if (spec) {
         __shared__ uint32_t h1[3 * HBINS];
+        // the sample's first-digit histogram in RS_SR replicas, lane l adding to replica l mod
+        // RS_SR (a padded stride: other banks): the exponents crowd a Gaussian row's keys into a
+        // few bins, and one histogram took ~64-way conflicted atomics, 7 us a launch
+        __shared__ uint32_t hs[RS_SR * (HBINS + 1)];
         const uint32_t gen = (uint32_t)gen_word & 7u;
-        for (int i = t; i < HBINS; i += RS_NT) h[i] = 0;
+        for (int i = t; i < RS_SR * (HBINS + 1); i += RS_NT) hs[i] = 0;
         for (int i = t; i < 3 * HBINS; i += RS_NT) h1[i] = 0;
         __syncthreads();
         {
+            uint32_t* hr = hs + (t % RS_SR) * (HBINS + 1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                atomicAdd(&h[(sa[q] & 0x7FFFFFFFu) >> 20], 1u);
-                atomicAdd(&h[(sb[q] & 0x7FFFFFFFu) >> 20], 1u);
+                atomicAdd(&hr[(sa[q] & 0x7FFFFFFFu) >> 20], 1u);
+                atomicAdd(&hr[(sb[q] & 0x7FFFFFFFu) >> 20], 1u);
             }
         }
         __syncthreads();
+        for (int i = t; i < HBINS; i += RS_NT) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int r = 0; r < RS_SR; ++r) c += hs[r * (HBINS + 1) + i];
+            h[i] = c;
+        }
+        __syncthreads();
+        RS_STAMP(5);
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 2                             // (cost probe: loads + the sample's digit)
+        if (h[t] == 0x7FFFFFFFu) out[0] = 1.f;
+        return;
+#endif
         uint32_t ab;
         const uint32_t rs = (uint32_t)min((int64_t)RS_SS, max((int64_t)1, (K * RS_SS + d / 2) / d));
         hist_find(h, rs, bs, ab, scratch);                               // the sample's digit (uniform)
         __syncthreads();
+        RS_STAMP(6);
         // the second digit's histograms for the first digits bs - 1 .. bs + 1, and the count of keys
         // whose first digit is above them: with the K-th key's first digit among the three, that is
         // all the merger needs for both digits (the contended first-digit histogram — the exponents
@@ -2723,46 +2849,85 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t k = __float_as_uint(e[q]) & km;
                     const uint32_t w = (k >> 20) - bs + 1u;
-                    if (w < 3u) atomicAdd(&h1[w * HBINS + ((k >> 9) & 0x7FFu)], 1u);
-                    else abv += (k >> 20) > bs + 1u ? 1u : 0u;
+                    abv += (k >> 20) > bs + 1u ? 1u : 0u;                // (branch-free: above the window)
+                    if (w < 3u) {
+                        atomicAdd(&h1[w * HBINS + ((k >> 9) & 0x7FFu)], 1u);
+                        winm |= 1u << u;
+                    }
                 }
             }
         }
+        RS_STAMP(7);
         abv = wave_sum(abv);
         if (t == 0) scratch[0] = 0;
         __syncthreads();
         if ((t & 63) == 0 && abv) atomicAdd(&scratch[0], abv);
         __syncthreads();
         RS_STAMP(1);
+        // the float4 with no element in the window: final if the guess hits (first digit above the
+        // window: kept, below: +0), stored while the round runs; a miss rewrites every float4 later
+        auto spec_store = [&]() {
+            if (!FLC_RS_SPECST) return;
+            const auto ro = out_rsrc();
+            // (opaque copies: the 16 per-float4 lane masks the compiler would otherwise compute
+            // once and keep for the later store loops spilled SGPRs through the whole kernel)
+            int uvx = uv;
+            uint32_t wmx = winm;
+            asm volatile("" : "+v"(uvx), "+v"(wmx));
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                if (u < uvx && !((wmx >> u) & 1u)) {
+                    const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                    uint32_t o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) o[q] = (mag_key(e[q]) >> 20) > bs + 1u ? __float_as_uint(e[q]) : 0u;
+                    const u4v ov = {o[0], o[1], o[2], o[3]};
+                    // (the float4's offset in the VGPR operand: 16 scalar offsets kept live here
+                    // spilled SGPRs through the whole kernel)
+                    __builtin_amdgcn_raw_buffer_store_b128(ov, ro, voff + (uint32_t)(u * RS_NT * 16), 0, FLC_RS_STPOL);
+                }
+            }
+        };
         uint32_t* gs = ctl + RS_HSPEC + tr.grp * 3 * HBINS;
         for (int i = t; i < 3 * HBINS; i += RS_NT)
             if (h1[i]) __hip_atomic_fetch_add(gs + i, h1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == 0 && scratch[0]) __hip_atomic_fetch_add(ctl + RS_ABV + 32 * tr.grp, scratch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++bar;
+        // (the speculative stores: by the waves 1.. of the workgroups that wait, while they wait —
+        // wave 0 polls, and a poll would queue behind stores of its own, so it stores all its
+        // float4 at the end; the merger's after its release, its loads not queued behind them)
+        if (FLC_RS_SPECST && t < 64) winm = 0xFFFFu;
         if (rs_arrive(tr, &flag_s, &gen_s, gen)) {
             // the merger: the three second-digit histograms summed (all loads in flight at once) with
             // their totals; the first digit is the one of the three where the count from the top
             // reaches K (else the guess missed: the rounds start from the first digit), the second
             // from its histogram — both digits in ONE round
             RS_STAMP(2);
+#ifdef FLC_RS_PRINT
+            stamp[13] = 1;
+#endif
+            // every replica word loaded at once (RS_NG x 3 x HBINS / RS_NT a thread, one round trip),
+            // then added into h1 (its own counts first cleared) by LDS atomics
             uint32_t* s0 = ctl + RS_HSPEC;
-            for (int i = t; i < HBINS; i += RS_NT) {
+            constexpr int ML = RS_NG * 3 * HBINS / RS_NT;
+            uint32_t mv[ML];
 #pragma unroll
-                for (int w = 0; w < 3; ++w) {
-                    uint32_t c = 0;
-                    const uint32_t* sw = s0 + w * HBINS + i;
+            for (int j = 0; j < ML; ++j) mv[j] = __hip_atomic_load(s0 + t + j * RS_NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t ar = t < RS_NG ? __hip_atomic_load(ctl + RS_ABV + 32 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            for (int i = t; i < 3 * HBINS; i += RS_NT) h1[i] = 0;
+            __syncthreads();
 #pragma unroll
-                    for (int r = 0; r < RS_NG; ++r)
-                        c += __hip_atomic_load(sw + r * 3 * HBINS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (i == 0 && bs + (uint32_t)w == 1u) c -= pad;         // the padding: first digit 0, second 0
-                    h1[w * HBINS + i] = c;
-                }
+            for (int j = 0; j < ML; ++j) {
+                const int i = (t + j * RS_NT) % (3 * HBINS);
+                if (mv[j]) atomicAdd(&h1[i], mv[j]);
             }
-            if (t == 0) {
-                uint32_t A = 0;
-#pragma unroll
-                for (int r = 0; r < RS_NG; ++r) A += __hip_atomic_load(ctl + RS_ABV + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                scratch[259] = A;
+            if (t < 64) {
+                const uint32_t a4 = wave_sum(ar);
+                if (t == 0) scratch[259] = a4;
+            }
+            __syncthreads();
+            if (t < 2) {                                                 // the padding: first digit 0, second 0
+                if (bs + (uint32_t)t == 1u) h1[t * HBINS] -= pad;
             }
             __syncthreads();
             const uint32_t A = scratch[259];
@@ -2780,22 +2945,29 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             }
             rs_release(tr, &gen_s, pl);
             if (t == 0) { scratch[0] = (uint32_t)pl; scratch[1] = (uint32_t)(pl >> 32); }
+            RS_STAMP(3);
+            spec_store();
             if (t < RS_NG) __hip_atomic_store(ctl + RS_ABV + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (int i = t; i < 3 * RS_NG * HBINS; i += RS_NT)           // clean for the next call
                 __hip_atomic_store(s0 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             RS_STAMP(2);
-            if (!rs_wait(tr, &gen_s, scratch, &ok_s, &rep_s, spin, seq)) goto leave;
+            spec_store();
+            if (!rs_wait(tr, &gen_s, scratch, &ok_s, &rep_s, spin, seq, true)) goto leave;
         }
-        __syncthreads();
+        // (raw barriers: a __syncthreads here would drain the speculative stores first)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         const uint64_t pl = ((uint64_t)scratch[1] << 32) | scratch[0];
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         if (pl & 1u) {
             prefix = (uint32_t)(pl >> 1) & 0x3FFFFFu;
             krem = (uint32_t)(pl >> 23) & 0xFFFFFFu;
             last = (uint32_t)(pl >> 47);
             p0 = 2;
             cand = last <= (uint32_t)RS_CAP;
+            sst = FLC_RS_SPECST;
         }                                                                // (else p0 = 0: the full rounds)
         RS_STAMP(3);
     }
@@ -2820,13 +2992,6 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         }
         __syncthreads();
         RS_STAMP(1 + 3 * p);
-#ifdef FLC_RS_PRINT
-        if (t == 0 && p == 0) {
-            uint64_t* pr = reinterpret_cast<uint64_t*>(ctl + RS_PROBE);
-            __hip_atomic_store(pr + g, stamp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(pr + 1024 + g, stamp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#endif
         uint32_t* gh = ctl + RS_HREP + (p * RS_NG + tr.grp) * HBINS;
         for (int i = t; i < HBINS; i += RS_NT)
             if (h[i]) __hip_atomic_fetch_add(gh + i, h[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2883,17 +3048,21 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                     nc += ((mag_key(e[q]) >> 9) == P && (int64_t)(f0 + u * RS_NT) * 4 + q < d) ? 1u : 0u;
             }
         }
+        RS_STAMP(8);
         uint32_t ctot;
         uint32_t pos = ex_scan<RS_NT>(nc, wsum, ctot);
-        if (ctot) {                                                      // (uniform)
-            if (t == 0) scratch[0] = __hip_atomic_fetch_add(ctl + RS_CCNT, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        RS_STAMP(9);
+        // the listed elements: the first RS_CS into this workgroup's own slots (no shared counter on
+        // the path: 245 returning adds on one word serialised ~3 us), any beyond them into the
+        // shared list at a reserved offset; the count into the workgroup's count word
+        uint32_t obase = 0;
+        if (ctot > (uint32_t)RS_CS) {                                    // (uniform)
+            if (t == 0) scratch[0] = __hip_atomic_fetch_add(ctl + RS_CCNT, ctot - (uint32_t)RS_CS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
-            pos += scratch[0];
+            obase = scratch[0];
         }
         uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
-        // the listed elements first: their stores are done at the arrival (rs_arrive waits for
-        // them); the dense output is stored after it, without the listed positions (the last
-        // workgroup writes those), so its 8 D bytes drain under the ranking instead of before it
+        uint64_t* cr = reinterpret_cast<uint64_t*>(ctl + RS_CREG) + (size_t)g * RS_CS;
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             if (u < uv) {
@@ -2902,17 +3071,26 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t j = (f0 + u * RS_NT) * 4u + (uint32_t)q;
                     if ((mag_key(e[q]) >> 9) == P && (int64_t)j < d) {
-                        if (pos < (uint32_t)RS_CAP)
-                            __hip_atomic_store(cl + pos, ((uint64_t)__float_as_uint(e[q]) << 32) | j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t en = ((uint64_t)__float_as_uint(e[q]) << 32) | j;
+                        if (pos < (uint32_t)RS_CS) __hip_atomic_store(cr + pos, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        else if (obase + pos - RS_CS < (uint32_t)RS_CAP)
+                            __hip_atomic_store(cl + obase + pos - RS_CS, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         ++pos;
                     }
                 }
             }
         }
+        if (t == 0) __hip_atomic_store(ctl + RS_CNUM + g, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the dense output without the listed positions (the ranking workgroup writes those); with
+        // the speculative stores made, only the float4 holding a window element are left
         auto dense = [&]() {
+            const auto ro = out_rsrc();
+            int uvx = uv;
+            uint32_t wmx = sst ? winm : 0xFFFFu;
+            asm volatile("" : "+v"(uvx), "+v"(wmx));
 #pragma unroll
             for (int u = 0; u < RU; ++u) {
-                if (u < uv) {
+                if (u < uvx && ((wmx >> u) & 1u)) {
                     const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
                     uint32_t o[4];
                     bool at[4], any = false;
@@ -2935,21 +3113,76 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             }
         };
         RS_STAMP(10);
-        if (rs_arrive(tr, &flag_s, &gen_s, 0u)) {
-            // the last workgroup: rank the m listed elements, store the krem first and +0 for the
-            // rest (then its own dense output).  Every workgroup arrived here, so no wait of the
-            // call gave up and none is left; a list that does not add up (never seen) aborts the
-            // call instead of storing anything doubtful, and the repair selects the row.
+        // every wave's list stores performed, then the workgroup counts out (its last hand-off) —
+        // except the ranking workgroup (the last one: its slice of the row is the shortest), which
+        // stores its dense output, waits until the others are out, then ranks the list
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (g != G - 1u) {
+            count_out();
+            dense();
+        } else {
+            dense();
+            // (everything below from the LDS copy of the arguments: kept in registers across the
+            // dense stores they spill SGPRs all through them)
+            const RsExit ex = ex_s;
+            if (t == 0) {
+                const uint64_t t0 = (uint64_t)wall_clock64();
+                uint32_t okw = 1;
+                for (;;) {
+                    uint32_t out_n = 0;
+#pragma unroll
+                    for (int r = 0; r < RS_NG; ++r)
+                        out_n += __hip_atomic_load(ex.ctl + RS_XGRP + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (out_n - ex.xbase >= ex.G - 1u) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((uint64_t)wall_clock64() - t0 > ex.spin) {                 // (never seen: all ran the round)
+                        if (__hip_atomic_exchange(ex.ctl + RS_GAVE, ex.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ex.seq) rep_s = 1;
+                        okw = 0;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");          // (compiler order only)
+                ok_s = okw;
+            }
+            __syncthreads();
+            if (!ok_s) goto leave;
+            // the list: every workgroup's count and slots (one thread each, all loads at once; slots
+            // beyond a count are stale and unused), then the shared list's overflow entries — m
+            // entries in all, every element at P (checked: a list that does not add up aborts the
+            // call and the repair selects the row), ranked by (key desc, tie order)
             __shared__ uint64_t comp[RS_CAP];
+            __shared__ uint64_t ent[RS_CAP];
             __shared__ uint64_t kth_s;
-            const uint32_t m = __hip_atomic_load(ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool ok = m == last && m >= krem && krem >= 1u && m <= (uint32_t)RS_CAP;   // every element at P listed
+            uint32_t c = 0;
+            uint64_t sl[RS_CS];
+            if (t < ex.G) {
+                c = __hip_atomic_load(ex.ctl + RS_CNUM + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t* ct = reinterpret_cast<const uint64_t*>(ex.ctl + RS_CREG) + (size_t)t * RS_CS;
+#pragma unroll
+                for (int k = 0; k < RS_CS; ++k) sl[k] = __hip_atomic_load(ct + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const uint32_t ov = t == 0 ? __hip_atomic_load(ex.ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            if (t == 0) scratch[4] = ov;
+            const uint32_t cs = min(c, (uint32_t)RS_CS);
+            uint32_t m, ns;
+            (void)ex_scan<RS_NT>(c, wsum, m);                            // (also the barrier before scratch[4])
+            const uint32_t sp = ex_scan<RS_NT>(cs, wsum, ns);
+            const uint32_t ovn = scratch[4];
+            const bool ok = m == last && ovn == m - ns && m >= krem && krem >= 1u && m <= (uint32_t)RS_CAP;
             const uint32_t mm = ok ? m : 0u;
-            for (uint32_t i = t; i < mm; i += RS_NT) {
-                const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                comp[i] = ((uint64_t)((uint32_t)(en >> 32) & 0x7FFFFFFFu) << 32) | tie_pref((uint32_t)en, ws.tie_hi);
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < RS_CS; ++k)
+                    if ((uint32_t)k < cs) ent[sp + k] = sl[k];
+                for (uint32_t i = t; i < ovn; i += RS_NT) ent[ns + i] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(ex.ctl + RS_CLIST) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (t == 0) { scratch[2] = 0; scratch[3] = 0; kth_s = ~0ull; }
+            __syncthreads();
+            for (uint32_t i = t; i < mm; i += RS_NT) {
+                const uint64_t en = ent[i];
+                comp[i] = ((uint64_t)((uint32_t)(en >> 32) & 0x7FFFFFFFu) << 32) | tie_pref((uint32_t)en, ex.tie_hi);
+            }
             __syncthreads();
             for (uint32_t i = t; i < mm; i += RS_NT) {
                 const uint64_t me = comp[i];
@@ -2962,29 +3195,28 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             const uint32_t kth = (uint32_t)(kc >> 32);
             for (uint32_t i = t; i < mm; i += RS_NT) {
                 const uint64_t me = comp[i];
-                const uint64_t en = __hip_atomic_load(cl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                out[(uint32_t)en] = me >= kc ? __uint_as_float((uint32_t)(en >> 32)) : 0.f;
+                const uint64_t en = ent[i];
+                ex.out[(uint32_t)en] = me >= kc ? __uint_as_float((uint32_t)(en >> 32)) : 0.f;
                 const uint32_t key = (uint32_t)(me >> 32);
                 if (key > kth) atomicAdd(&scratch[2], 1u);
                 else if (key == kth) atomicAdd(&scratch[3], 1u);
             }
             __syncthreads();
             if (t == 0) {
-                __hip_atomic_store(ctl + RS_CCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // clean for the next call
+                if (ovn) __hip_atomic_store(ex.ctl + RS_CCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // clean for the next call
                 const uint32_t gt = scratch[2], eq = scratch[3];
-                ws.thr[0] = kth;
-                ws.krem[0] = krem - gt;
-                ws.tiecut[0] = tie_pref((uint32_t)kc, ws.tie_hi);
-                ws.flags[0] = F_RESIDENT | (gt + eq > krem ? F_TIES : 0u);
-                if (!ok && __hip_atomic_exchange(ctl + RS_GAVE, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq)
+                *ex.thr = kth;
+                *ex.krem = krem - gt;
+                *ex.tiecut = tie_pref((uint32_t)kc, ex.tie_hi);
+                *ex.flags = F_RESIDENT | (gt + eq > krem ? F_TIES : 0u);
+                if (!ok && __hip_atomic_exchange(ex.ctl + RS_GAVE, ex.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ex.seq)
                     rep_s = 1;
             }
             if (!ok) goto leave;                                         // (uniform) aborted: repaired
-            count_out();
-            dense();
-        } else {
-            count_out();
-            dense();
+            if (t == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_fetch_add(ex.ctl + RS_XGRP + 32 * (blockIdx.x % RS_NG), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         RS_STAMP(11);
     } else {
@@ -3060,17 +3292,32 @@ store:
     // counted out, so that a repair's later state is the one that stays), counted out, then the
     // stores (final values)
     if (g == 0 && t == 0) {
+#if FLC_RS_FENCE
         ws.thr[0] = thr;
         ws.krem[0] = krem;
         ws.tiecut[0] = 0;
         ws.flags[0] = F_RESIDENT | (tie_cut ? F_TIES : 0u);
         if (FLC_RS_G0REL) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
+        // written through (agent-scope stores) and drained before the count-out, so that a
+        // repair's later row state is the one that stays
+        __hip_atomic_store(ws.thr, thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws.krem, krem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws.tiecut, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws.flags, F_RESIDENT | (tie_cut ? F_TIES : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     }
     count_out();
-    // the dense output from the registers: x where kept, +0 elsewhere (range-checked: no padding)
+    // the dense output from the registers: x where kept, +0 elsewhere (range-checked: no padding);
+    // with the speculative stores made, only the float4 holding a window element
+    const auto ro = out_rsrc();
+    int uvx = uv;
+    uint32_t wmx = sst ? winm : 0xFFFFu;
+    asm volatile("" : "+v"(uvx), "+v"(wmx));
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-        if (u < uv) {
+        if (u < uvx && ((wmx >> u) & 1u)) {
             const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
             uint32_t o[4];
 #pragma unroll
@@ -3119,30 +3366,16 @@ leave:
         if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         count_out();
     }
-done:
+done:;
 #ifdef FLC_RS_PRINT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     RS_STAMP(12);
-    if (g == 0 && t == 0) {
-        const uint64_t* pr = reinterpret_cast<const uint64_t*>(ctl + RS_PROBE);
-        uint64_t smax = 0, amax = 0, smin = ~0ull;
-        uint32_t gs = 0, ga = 0;
-        for (uint32_t i = 0; i < G; ++i) {
-            const uint64_t s0 = __hip_atomic_load(pr + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t a0 = __hip_atomic_load(pr + 1024 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            smin = s0 < smin ? s0 : smin;
-            if (s0 > smax) { smax = s0; gs = i; }
-            if (a0 > amax) { amax = a0; ga = i; }
-        }
-        printf("rs_skew: start spread %llu (last wg %u), last pass-0 hist done at %llu (wg %u, its own %llu) after wg 0 start\n",
-               smax - smin, gs, amax - stamp[0], ga, amax - __hip_atomic_load(pr + ga, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (t == 0 && G <= 256u) {
+        uint64_t* pr = reinterpret_cast<uint64_t*>(ex_s.ctl + RS_PROBE);
+        const int ks[8] = {FLC_RS_TLK, 13};
+        for (int k = 0; k < 8; ++k) __hip_atomic_store(pr + k * 256 + g, stamp[ks[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (g == 0 && t == 0)
-        printf("rs_stamps G=%u e4=%d NG=%d: load+h0 %llu arrive0 %llu wait0 %llu | h1 %llu arrive1 %llu wait1 %llu | h2 %llu arrive2 %llu wait2 %llu | tie %llu store %llu drain %llu (x10ns)\n",
-               G, e4, RS_NG, stamp[1] - stamp[0], stamp[2] - stamp[1], stamp[3] - stamp[2], stamp[4] - stamp[3], stamp[5] - stamp[4],
-               stamp[6] - stamp[5], stamp[7] - stamp[6], stamp[8] - stamp[7], stamp[9] - stamp[8], stamp[10] - stamp[9],
-               stamp[11] - stamp[10], stamp[12] - stamp[11]);
 #endif
 }
 

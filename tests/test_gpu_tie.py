@@ -293,3 +293,30 @@ def test_compressvector_under_graph_capture(ag):
         graph.replay()
         torch.cuda.synchronize()
         np.testing.assert_array_equal(_bits(out), want)
+
+
+@pytest.mark.parametrize("tie", ["lowest", "highest"])
+def test_compressvector_resident_list_overflow(ag, tie):
+    """k_lone_resident's candidate finish lists the elements sharing the K-th key's 22-bit prefix:
+    each workgroup's first RS_CS (4) in slots of its own, any beyond them in the shared list at an
+    offset it reserves.  A row whose prefix group (~700 elements, some exactly tied) sits mostly in
+    the first workgroup's slice (600 of them) and partly in another's drives both stores and the
+    ranking workgroup's merge of the two: bit-exact vs the oracle, no abort, no repair."""
+    d, k = 10_000_000, 100_000
+    g = np.random.default_rng(4242)
+    x = g.standard_normal(d).astype(np.float32)
+    v = np.sort(np.abs(x))[::-1][k - 1 - 300]
+    base = np.float32(v).view(np.uint32) & np.uint32(0xFFFFFE00)      # the 22-bit prefix of v
+    low = g.integers(0, 512, 650).astype(np.uint32)
+    low[::50] = low[0]                                                  # a few exact ties
+    mags = (base | low).view(np.float32)
+    small = np.abs(x) < 1.0
+    first = np.flatnonzero(small[:30_000])[:600]                       # workgroup 0's slice
+    other = np.flatnonzero(small[4_000_000:4_030_000])[:50] + 4_000_000
+    pos = np.concatenate([first, other])
+    x[pos] = mags * np.where(g.random(pos.size) < 0.5, -1.0, 1.0).astype(np.float32)
+    xt = torch.from_numpy(x).cuda()
+    c = _comp(ag, f"topk:{k}", d, tie)
+    np.testing.assert_array_equal(_bits(c.compressVector(xt)), _bits(_enc([x], k, tie)[0]), err_msg=tie)
+    f = int(ag.select_row_flags(c, 1, d)[0])
+    assert f & 16 and not f & 1 and not f & 32, f"{tie}: flags {f}"
