@@ -64,7 +64,10 @@ constexpr int RS_XGRP = RS_GRP + 32 * RS_NG_MAX;  // per group: workgroups count
 constexpr int RS_ABV = RS_XGRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
 constexpr int RS_SS = 8192;           // the speculative first digit's sample (32 pieces of 256)
-constexpr int RS_SR = 8;              // replicas of the sample's histogram (LDS)
+#ifndef FLC_RS_SR
+#define FLC_RS_SR 1                   // replicas of the sample's histogram (LDS; 8 measured 0.35 us slower a call)
+#endif
+constexpr int RS_SR = FLC_RS_SR;
 #ifndef FLC_RS_STPOL
 #define FLC_RS_STPOL 2                // the dense output's stores: nontemporal (2) or default (0)
 #endif
@@ -156,6 +159,19 @@ __device__ __host__ inline uint32_t tie_all(uint32_t hi) { return hi ? 0u : 0xFF
 // Find, scanning a 2048-bin histogram from the TOP bin down, the bin b where the running count
 // reaches k (1-based).  Returns b and the count strictly above b.  256 threads, 8 bins each.
 // (t, own): the thread's index in the 256 that scan; every thread of the block takes the barriers.
+// A workgroup barrier for LDS only: this wave's LDS operations done, then s_barrier — unlike
+// __syncthreads it does not wait for the wave's global loads (vmcnt), so loads stay in flight.
+__device__ inline void lds_bar() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+template <bool RAW>
+__device__ inline void blk_bar() {
+    if (RAW) lds_bar();
+    else __syncthreads();
+}
+template <bool RAW = false>
 __device__ inline void hist_find_at(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
                                     uint32_t* scratch /* LDS 256+2 */, int t, bool own) {
     // thread t owns bins [HBINS-8(t+1), HBINS-8t)  (top bins first)
@@ -174,7 +190,7 @@ __device__ inline void hist_find_at(const uint32_t* h, uint32_t k, uint32_t& bin
         inc += lane >= off ? v : 0u;
     }
     if (own && lane == 63) scratch[w] = inc;
-    __syncthreads();
+    blk_bar<RAW>();
     uint32_t before = 0;
     if (own)
         for (int q = 0; q < w; ++q) before += scratch[q];
@@ -191,10 +207,10 @@ __device__ inline void hist_find_at(const uint32_t* h, uint32_t k, uint32_t& bin
             run += local[q];
         }
     }
-    __syncthreads();
+    blk_bar<RAW>();
     bin = scratch[256];
     above = scratch[257];
-    __syncthreads();
+    blk_bar<RAW>();
 }
 // The same search over NB bins (NB / 256 a thread, threads 0..255 of a larger block; the rest only
 // sync); found = false when the bins hold fewer than k in all.
@@ -242,9 +258,10 @@ __device__ inline void hist_find_n(const uint32_t* h, uint32_t k, uint32_t& bin,
     found = scratch[258] != 0u;
     __syncthreads();
 }
+template <bool RAW = false>
 __device__ inline void hist_find(const uint32_t* h, uint32_t k, uint32_t& bin, uint32_t& above,
                                  uint32_t* scratch /* LDS 256+2 */) {
-    hist_find_at(h, k, bin, above, scratch, (int)threadIdx.x, threadIdx.x < 256);   // larger blocks: the rest only sync
+    hist_find_at<RAW>(h, k, bin, above, scratch, (int)threadIdx.x, threadIdx.x < 256);   // larger blocks: the rest only sync
 }
 // Two searches side by side (blocks of >= 512 threads): threads 0-255 scan ha for ka, 256-511 hb for kb.
 __device__ inline void hist_find2(const uint32_t* ha, uint32_t ka, uint32_t& bina, uint32_t& abovea, uint32_t* sa,
@@ -2656,7 +2673,7 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     __shared__ uint32_t flag_s, gen_s, ok_s;
     const uint32_t G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
 #ifdef FLC_RS_PRINT
-    uint64_t stamp[16] = {0};
+    uint64_t stamp[18] = {0};
     // every 16th call, workgroup 0 summarises the PREVIOUS call's per-workgroup timeline (complete:
     // that launch has ended), so that the stamps are of back-to-back calls, not of a cold launch
     if (g == 0 && t == 0 && (seq & 15u) == 0u && G <= 256u) {
@@ -2763,8 +2780,10 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         v[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]));
     }
 #ifdef FLC_RS_PRINT
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                    // (probe: when the row has landed)
-    RS_STAMP(4);
+    if (t < 64) {                                                        // (probe: when wave 0's row has landed)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RS_STAMP(4);
+    }
 #endif
 #if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 3                             // (cost probe: the loads, then the row stored)
     {
@@ -2801,13 +2820,15 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     if (spec) {
         __shared__ uint32_t h1[3 * HBINS];
         // the sample's first-digit histogram in RS_SR replicas, lane l adding to replica l mod
-        // RS_SR (a padded stride: other banks): the exponents crowd a Gaussian row's keys into a
-        // few bins, and one histogram took ~64-way conflicted atomics, 7 us a launch
+        // RS_SR (a padded stride: other banks) — the exponents crowd a Gaussian row's keys into a
+        // few bins; but the conflicts are not on the path (8 replicas: 0.35 us slower a call)
         __shared__ uint32_t hs[RS_SR * (HBINS + 1)];
         const uint32_t gen = (uint32_t)gen_word & 7u;
+        // (LDS-only barriers up to the row's histogram: the sample's digit is picked while the
+        // row's loads are still in flight — a __syncthreads waits for them, ~7 us)
         for (int i = t; i < RS_SR * (HBINS + 1); i += RS_NT) hs[i] = 0;
         for (int i = t; i < 3 * HBINS; i += RS_NT) h1[i] = 0;
-        __syncthreads();
+        lds_bar();
         {
             uint32_t* hr = hs + (t % RS_SR) * (HBINS + 1);
 #pragma unroll
@@ -2816,14 +2837,14 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 atomicAdd(&hr[(sb[q] & 0x7FFFFFFFu) >> 20], 1u);
             }
         }
-        __syncthreads();
+        lds_bar();
         for (int i = t; i < HBINS; i += RS_NT) {
             uint32_t c = 0;
 #pragma unroll
             for (int r = 0; r < RS_SR; ++r) c += hs[r * (HBINS + 1) + i];
             h[i] = c;
         }
-        __syncthreads();
+        lds_bar();
         RS_STAMP(5);
 #if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 2                             // (cost probe: loads + the sample's digit)
         if (h[t] == 0x7FFFFFFFu) out[0] = 1.f;
@@ -2831,8 +2852,8 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
 #endif
         uint32_t ab;
         const uint32_t rs = (uint32_t)min((int64_t)RS_SS, max((int64_t)1, (K * RS_SS + d / 2) / d));
-        hist_find(h, rs, bs, ab, scratch);                               // the sample's digit (uniform)
-        __syncthreads();
+        hist_find<true>(h, rs, bs, ab, scratch);                         // the sample's digit (uniform)
+        lds_bar();
         RS_STAMP(6);
         // the second digit's histograms for the first digits bs - 1 .. bs + 1, and the count of keys
         // whose first digit is above them: with the K-th key's first digit among the three, that is
