@@ -27,6 +27,7 @@ timeout -k 10 400 python tools/collect_pmc.py --dropin --workload c3 --n 8 --ste
 timeout -k 10 400 python tools/collect_pmc.py --dropin --workload c4 --n 4 --steps 5 > $out/pmc_dropin_c4.log 2>&1 || exit $?
 echo "pmc done"
 fi
+[ -n "$EV_STOP_AFTER_PMC" ] && exit 0
 for wl in c3 c4 c2 c5; do
   st=20; wu=3; [ $wl = c5 ] && { st=5; wu=2; }
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $out/stats_$wl -o run --output-format csv -- \
