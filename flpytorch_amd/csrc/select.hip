@@ -77,6 +77,9 @@ constexpr int RS_SR = FLC_RS_SR;
 #ifndef FLC_RS_POLLAB
 #define FLC_RS_POLLAB 1               // k_lone_resident: a grid wait reads the abort word every n-th poll
 #endif
+#ifndef FLC_RS_RANKFIRST
+#define FLC_RS_RANKFIRST 0            // 1: the ranking workgroup ranks before its own dense stores (measured 0.2 us slower)
+#endif
 #ifndef FLC_RS_PROBE_NOCOUNT
 #define FLC_RS_PROBE_NOCOUNT 0        // (cost probes only: no exit count — an aborted call would not repair)
 #endif
@@ -2670,7 +2673,8 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     __shared__ uint32_t h[HBINS];
     __shared__ uint32_t scratch[260];
     __shared__ uint32_t wsum[RS_NT / 64];
-    __shared__ uint32_t flag_s, gen_s, ok_s;
+    __shared__ uint32_t flag_s, gen_s, ok_s, lcnt_s;
+    __shared__ uint64_t lst[RS_CAP];                                     // this workgroup's listed elements
     const uint32_t G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
 #ifdef FLC_RS_PRINT
     uint64_t stamp[18] = {0};
@@ -2727,6 +2731,7 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
     __shared__ uint32_t rep_s;                                          // 1: this workgroup repairs the call
     if (t == 0) {
         rep_s = 0;
+        lcnt_s = 0;
         ex_s = RsExit{rows.row_s(0), out, ctl, ws.thr, ws.krem, ws.tiecut, ws.flags, (uint32_t)d, (uint32_t)K, ws.tie_hi, seq,
                       G, xbase, spin};
     }
@@ -2861,7 +2866,11 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         // crowd into few bins — is not built at all unless the guess misses)
         uint32_t km = 0x7FFFFFFFu;
         asm volatile("" : "+s"(km));
-        uint32_t abv = 0;
+        // (per element: the key, its offset from the window's low end, one compare into the
+        // histogram's exec mask, one into a ballot counted by the scalar unit — every VALU op a
+        // row element costs is ~0.25 us of a launch with one 16-wave workgroup per CU)
+        const uint32_t wlo = (bs - 1u) << 20, whi = (bs + 2u) << 20;   // the window: first digits bs-1 .. bs+1
+        uint32_t abv = 0;                                                // keys above the window (wave total)
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             if (u < uv) {
@@ -2869,22 +2878,25 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t k = __float_as_uint(e[q]) & km;
-                    const uint32_t w = (k >> 20) - bs + 1u;
-                    abv += (k >> 20) > bs + 1u ? 1u : 0u;                // (branch-free: above the window)
-                    if (w < 3u) {
-                        atomicAdd(&h1[w * HBINS + ((k >> 9) & 0x7FFu)], 1u);
+                    const uint32_t dd = k - wlo;                         // window bin = dd >> 9 (3 x 2048)
+                    abv += (uint32_t)__popcll(__ballot(k >= whi));
+                    if (dd < (3u << 20)) {
+                        atomicAdd(&h1[dd >> 9], 1u);
                         winm |= 1u << u;
                     }
                 }
             }
         }
         RS_STAMP(7);
-        abv = wave_sum(abv);
         if (t == 0) scratch[0] = 0;
         __syncthreads();
         if ((t & 63) == 0 && abv) atomicAdd(&scratch[0], abv);
         __syncthreads();
         RS_STAMP(1);
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 4                             // (cost probe: + the window histograms)
+        if (scratch[0] == 0x7FFFFFFFu) out[0] = 1.f;
+        return;
+#endif
         // the float4 with no element in the window: final if the guess hits (first digit above the
         // window: kept, below: +0), stored while the round runs; a miss rewrites every float4 later
         auto spec_store = [&]() {
@@ -2918,7 +2930,11 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         // wave 0 polls, and a poll would queue behind stores of its own, so it stores all its
         // float4 at the end; the merger's after its release, its loads not queued behind them)
         if (FLC_RS_SPECST && t < 64) winm = 0xFFFFu;
-        if (rs_arrive(tr, &flag_s, &gen_s, gen)) {
+        const bool mg_ = rs_arrive(tr, &flag_s, &gen_s, gen);
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 5                             // (cost probe: + the flush and the arrival)
+        return;
+#endif
+        if (mg_) {
             // the merger: the three second-digit histograms summed (all loads in flight at once) with
             // their totals; the first digit is the one of the three where the count from the top
             // reaches K (else the guess missed: the rounds start from the first digit), the second
@@ -2989,7 +3005,10 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             p0 = 2;
             cand = last <= (uint32_t)RS_CAP;
             sst = FLC_RS_SPECST;
-        }                                                                // (else p0 = 0: the full rounds)
+        }
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 6                             // (cost probe: + the merger and the release)
+        return;
+#endif                                                                // (else p0 = 0: the full rounds)
         RS_STAMP(3);
     }
     for (int p = p0; p < 3 && !cand; ++p) {
@@ -3059,49 +3078,48 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         // The third digit's round and the tie counts' exchange are not needed; nobody waits for the
         // ranking.  (The padding of the straddling float4 is never listed.)
         const uint32_t P = prefix;
-        uint32_t nc = 0;
-#pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            if (u < uv) {
-                const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    nc += ((mag_key(e[q]) >> 9) == P && (int64_t)(f0 + u * RS_NT) * 4 + q < d) ? 1u : 0u;
-            }
-        }
-        RS_STAMP(8);
-        uint32_t ctot;
-        uint32_t pos = ex_scan<RS_NT>(nc, wsum, ctot);
-        RS_STAMP(9);
-        // the listed elements: the first RS_CS into this workgroup's own slots (no shared counter on
-        // the path: 245 returning adds on one word serialised ~3 us), any beyond them into the
-        // shared list at a reserved offset; the count into the workgroup's count word
-        uint32_t obase = 0;
-        if (ctot > (uint32_t)RS_CS) {                                    // (uniform)
-            if (t == 0) scratch[0] = __hip_atomic_fetch_add(ctl + RS_CCNT, ctot - (uint32_t)RS_CS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            obase = scratch[0];
-        }
-        uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
-        uint64_t* cr = reinterpret_cast<uint64_t*>(ctl + RS_CREG) + (size_t)g * RS_CS;
+        const uint32_t plo = P << 9;                                     // keys at P: [plo, plo + 512)
+        // the listed elements into this workgroup's LDS list at positions from an LDS counter
+        // (~70 in a 10 M row: the rare atomics cost less than a counting pass and a scan over
+        // every element), then wave 0 hands them over: the first RS_CS into this workgroup's own
+        // slots (no shared counter on the path: 245 returning adds on one word serialised ~3 us),
+        // any beyond them into the shared list at a reserved offset, the count into its count word
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             if (u < uv) {
                 const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const uint32_t j = (f0 + u * RS_NT) * 4u + (uint32_t)q;
-                    if ((mag_key(e[q]) >> 9) == P && (int64_t)j < d) {
-                        const uint64_t en = ((uint64_t)__float_as_uint(e[q]) << 32) | j;
-                        if (pos < (uint32_t)RS_CS) __hip_atomic_store(cr + pos, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        else if (obase + pos - RS_CS < (uint32_t)RS_CAP)
-                            __hip_atomic_store(cl + obase + pos - RS_CS, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ++pos;
+                    if (mag_key(e[q]) - plo < 512u) {
+                        const uint32_t j = (f0 + u * RS_NT) * 4u + (uint32_t)q;
+                        if ((int64_t)j < d) {                            // (not the straddling float4's padding)
+                            const uint32_t pp = atomicAdd(&lcnt_s, 1u);
+                            if (pp < (uint32_t)RS_CAP) lst[pp] = ((uint64_t)__float_as_uint(e[q]) << 32) | j;
+                        }
                     }
                 }
             }
         }
-        if (t == 0) __hip_atomic_store(ctl + RS_CNUM + g, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lds_bar();
+        const uint32_t ctot = lcnt_s;                                    // (uniform)
+        RS_STAMP(9);
+        if (t < 64) {
+            uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
+            uint64_t* cr = reinterpret_cast<uint64_t*>(ctl + RS_CREG) + (size_t)g * RS_CS;
+            uint32_t ob = 0;
+            if (ctot > (uint32_t)RS_CS && t == 0)
+                ob = __hip_atomic_fetch_add(ctl + RS_CCNT, ctot - (uint32_t)RS_CS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t obase = __shfl(ob, 0, 64);
+            const uint32_t nl = min(ctot, (uint32_t)RS_CAP);
+            for (uint32_t i = t; i < nl; i += 64) {
+                const uint64_t en = lst[i];
+                if (i < (uint32_t)RS_CS) __hip_atomic_store(cr + i, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (obase + i - RS_CS < (uint32_t)RS_CAP)
+                    __hip_atomic_store(cl + obase + i - RS_CS, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (t == 0) __hip_atomic_store(ctl + RS_CNUM + g, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         // the dense output without the listed positions (the ranking workgroup writes those); with
         // the speculative stores made, only the float4 holding a window element are left
         auto dense = [&]() {
@@ -3117,9 +3135,9 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                     bool at[4], any = false;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const uint32_t kp = mag_key(e[q]) >> 9;
-                        o[q] = kp > P ? __float_as_uint(e[q]) : 0u;
-                        at[q] = kp == P;
+                        const uint32_t k = mag_key(e[q]);
+                        o[q] = k >= plo + 512u ? __float_as_uint(e[q]) : 0u;
+                        at[q] = k - plo < 512u;
                         any |= at[q];
                     }
                     if (!any) {
@@ -3134,16 +3152,19 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             }
         };
         RS_STAMP(10);
-        // every wave's list stores performed, then the workgroup counts out (its last hand-off) —
-        // except the ranking workgroup (the last one: its slice of the row is the shortest), which
-        // stores its dense output, waits until the others are out, then ranks the list
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        // the hand-over drained (wave 0), then the workgroup counts out (its last hand-off) and
+        // every wave stores its dense output — except the ranking workgroup (the last one: its
+        // slice of the row is the shortest), which stores its dense output, waits until the
+        // others are out, then ranks the list
         if (g != G - 1u) {
             count_out();
+            lds_bar();                                                   // (nothing stored before the count-out)
+#if defined(FLC_RS_EXIT) && FLC_RS_EXIT == 7                             // (cost probe: all but the others' dense stores)
+            return;
+#endif
             dense();
         } else {
-            dense();
+            if (!FLC_RS_RANKFIRST) dense();
             // (everything below from the LDS copy of the arguments: kept in registers across the
             // dense stores they spill SGPRs all through them)
             const RsExit ex = ex_s;
@@ -3238,6 +3259,7 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_fetch_add(ex.ctl + RS_XGRP + 32 * (blockIdx.x % RS_NG), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            if (FLC_RS_RANKFIRST) dense();
         }
         RS_STAMP(11);
     } else {
