@@ -4,7 +4,7 @@
 # non-ranking workgroups' dense stores; cur the whole call
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-o=gpurun_out/r06_exit3; mkdir -p $o
+o=gpurun_out/r06_exit4; mkdir -p $o
 for v in cur ex4 ex5 ex6 ex7; do
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $o/$v -o run --output-format csv -- python tools/ab_lone.py --variants $v --n 32 --rounds 2 > $o/$v.log 2>&1 || exit 1
   f=$(find $o/$v -name '*kernel_stats.csv' | head -1)
