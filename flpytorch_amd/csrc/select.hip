@@ -59,7 +59,7 @@ constexpr int RS_NG_MAX = 16;
 static_assert(RS_NG >= 1 && RS_NG <= RS_NG_MAX, "FLC_RS_NG: 1..16 groups");
 // its control words: counters on lines of their own, per-group digit histograms, tie counts
 // (RS_GAVE: the sequence number of a call that was aborted; RS_XGRP: workgroups that have left)
-constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_GRP = 128;
+constexpr int RS_GLOB = 0, RS_GEN = 32, RS_GAVE = 64, RS_CCNT = 96, RS_CDONE = 112, RS_GRP = 128;
 constexpr int RS_XGRP = RS_GRP + 32 * RS_NG_MAX;  // per group: workgroups counted out (runs on across calls)
 constexpr int RS_ABV = RS_XGRP + 32 * RS_NG_MAX;   // per group: keys above the speculated first digits
 constexpr int RS_CAP = 2048;          // candidates (22-bit prefix of the K-th key) ranked by the last workgroup
@@ -76,6 +76,14 @@ constexpr int RS_SR = FLC_RS_SR;
 #endif
 #ifndef FLC_RS_POLLAB
 #define FLC_RS_POLLAB 1               // k_lone_resident: a grid wait reads the abort word every n-th poll
+#endif
+#ifndef FLC_RS_DONE
+// k_lone_resident's candidate hand-over: 1 = a workgroup holding candidates reserves their place in
+// the shared list (one returning add), stores them and then adds their number to a delivered count;
+// the ranking workgroup waits for that count to reach the candidates' total (known to all from the
+// round's payload), not for every workgroup to count out, and reads the list in one pass.
+// 0 = per-workgroup slots gathered after every workgroup counted out.
+#define FLC_RS_DONE 1
 #endif
 #ifndef FLC_RS_RANKFIRST
 #define FLC_RS_RANKFIRST 0            // 1: the ranking workgroup ranks before its own dense stores (measured 0.2 us slower)
@@ -3103,7 +3111,19 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
         lds_bar();
         const uint32_t ctot = lcnt_s;                                    // (uniform)
         RS_STAMP(9);
-        if (t < 64) {
+        if (FLC_RS_DONE && t < 64 && ctot) {
+            // (the workgroups without candidates — nearly all — store nothing here)
+            uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
+            uint32_t ob = 0;
+            if (t == 0) ob = __hip_atomic_fetch_add(ctl + RS_CCNT, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t obase = __shfl(ob, 0, 64);
+            const uint32_t nl = min(ctot, (uint32_t)RS_CAP);
+            for (uint32_t i = t; i < nl; i += 64)
+                if (obase + i < (uint32_t)RS_CAP) __hip_atomic_store(cl + obase + i, lst[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t == 0) __hip_atomic_fetch_add(ctl + RS_CDONE, ctot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!FLC_RS_DONE && t < 64) {
             uint64_t* cl = reinterpret_cast<uint64_t*>(ctl + RS_CLIST);
             uint64_t* cr = reinterpret_cast<uint64_t*>(ctl + RS_CREG) + (size_t)g * RS_CS;
             uint32_t ob = 0;
@@ -3172,11 +3192,17 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
                 const uint64_t t0 = (uint64_t)wall_clock64();
                 uint32_t okw = 1;
                 for (;;) {
-                    uint32_t out_n = 0;
+                    if (FLC_RS_DONE) {
+                        // (every candidate delivered; more than `last` would be a list that does
+                        // not add up: the check below aborts it)
+                        if (__hip_atomic_load(ex.ctl + RS_CDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= last) break;
+                    } else {
+                        uint32_t out_n = 0;
 #pragma unroll
-                    for (int r = 0; r < RS_NG; ++r)
-                        out_n += __hip_atomic_load(ex.ctl + RS_XGRP + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (out_n - ex.xbase >= ex.G - 1u) break;
+                        for (int r = 0; r < RS_NG; ++r)
+                            out_n += __hip_atomic_load(ex.ctl + RS_XGRP + 32 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (out_n - ex.xbase >= ex.G - 1u) break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                     if ((uint64_t)wall_clock64() - t0 > ex.spin) {                 // (never seen: all ran the round)
                         if (__hip_atomic_exchange(ex.ctl + RS_GAVE, ex.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ex.seq) rep_s = 1;
@@ -3196,6 +3222,23 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             __shared__ uint64_t comp[RS_CAP];
             __shared__ uint64_t ent[RS_CAP];
             __shared__ uint64_t kth_s;
+            uint32_t m, ns, ovn, mm;
+            bool ok;
+            if (FLC_RS_DONE) {
+                // the shared list holds exactly the `last` candidates (delivered count and reserved
+                // count agree), read in one pass
+                if (t == 0) {
+                    scratch[4] = __hip_atomic_load(ex.ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    scratch[5] = __hip_atomic_load(ex.ctl + RS_CDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __syncthreads();
+                m = scratch[4];
+                ok = m == last && scratch[5] == last && m >= krem && krem >= 1u && m <= (uint32_t)RS_CAP;
+                mm = ok ? m : 0u;
+                for (uint32_t i = t; i < mm; i += RS_NT)
+                    ent[i] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(ex.ctl + RS_CLIST) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ovn = 1u;                                                // (the reserved count to reset below)
+            } else {
             uint32_t c = 0;
             uint64_t sl[RS_CS];
             if (t < ex.G) {
@@ -3207,17 +3250,17 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             const uint32_t ov = t == 0 ? __hip_atomic_load(ex.ctl + RS_CCNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
             if (t == 0) scratch[4] = ov;
             const uint32_t cs = min(c, (uint32_t)RS_CS);
-            uint32_t m, ns;
             (void)ex_scan<RS_NT>(c, wsum, m);                            // (also the barrier before scratch[4])
             const uint32_t sp = ex_scan<RS_NT>(cs, wsum, ns);
-            const uint32_t ovn = scratch[4];
-            const bool ok = m == last && ovn == m - ns && m >= krem && krem >= 1u && m <= (uint32_t)RS_CAP;
-            const uint32_t mm = ok ? m : 0u;
+            ovn = scratch[4];
+            ok = m == last && ovn == m - ns && m >= krem && krem >= 1u && m <= (uint32_t)RS_CAP;
+            mm = ok ? m : 0u;
             if (ok) {
 #pragma unroll
                 for (int k = 0; k < RS_CS; ++k)
                     if ((uint32_t)k < cs) ent[sp + k] = sl[k];
                 for (uint32_t i = t; i < ovn; i += RS_NT) ent[ns + i] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(ex.ctl + RS_CLIST) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             }
             if (t == 0) { scratch[2] = 0; scratch[3] = 0; kth_s = ~0ull; }
             __syncthreads();
@@ -3246,6 +3289,7 @@ __global__ __launch_bounds__(RS_NT) void k_lone_resident(RowSrc rows, int64_t d,
             __syncthreads();
             if (t == 0) {
                 if (ovn) __hip_atomic_store(ex.ctl + RS_CCNT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // clean for the next call
+                if (FLC_RS_DONE) __hip_atomic_store(ex.ctl + RS_CDONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t gt = scratch[2], eq = scratch[3];
                 *ex.thr = kth;
                 *ex.krem = krem - gt;
